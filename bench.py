@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: Krylov iterations/sec of the tensor-Krylov inner iteration on MI355X.
+
+Workload (BASELINE.json configs[2], SURVEY.md 8d "C2"): d = 8 factors, n_s = 2^20
+tridiagonal Laplacian (assemble_matrix(n, Laplace), src/tensor_struct.jl:48-57), fp64,
+distinct b_s ~ U(0,1) (seed 1000+s) normalized, K = nmax = 50, TensorArnoldi (SpMV +
+two-pass MGS per factor, src/orthogonal_bases.jl:15-37).
+
+One bench "step" = one full device sweep of the iteration: V[:,1] = b/|b|, then the
+K = 50 orthonormalize!(td, k) iterations over all d factors (k = 1..50; each one the
+SpMV + MGS2 step of every factor plus update_rhs!'s <V_k, b_s> and factor 1's Gram
+row), with the per-iteration RCCL all-reduce of the factors' records when N > 1, and
+the final basis_tensor_mul! X_s = V_s Y_s (t = the exp-sum rank at k = 50) on MFMA.
+Inputs are resident in HBM before timing.  value = K * steps / time (whole job).
+Factors are partitioned over ranks (one process per GPU): the total work is fixed, so
+the scaling is STRONG (see DESIGN.md "Multi-GPU").
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
+       (N > 1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "tensorkrylov.jl_amd"))
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+FP64_MFMA_PEAK_TF = 78.6
+
+CONFIGS = {
+    # name: (d, n, matrix class, method, K, instance)
+    "C1": (4, 1 << 18, "Laplace", "TensorArnoldi", 50, "SymInstance"),
+    "C2": (8, 1 << 20, "Laplace", "TensorArnoldi", 50, "SymInstance"),
+    "C3": (5, 1 << 19, "RandSparseSPD", "TensorArnoldi", 50, "SymInstance"),
+    "C4": (10, 1 << 17, "ConvDiff", "TensorArnoldi", 50, "NonSymInstance"),
+}
+
+
+def alg_bytes_step(n, nnz, k):
+    """algorithmic bytes of one Arnoldi factor-step with k basis columns
+    (int32 CSR): B_spmv + 2 MGS passes + write V_{k+1} + the RHS dot."""
+    b_spmv = 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n
+    return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    import tkamd
+    from tkamd import _lib as L
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+
+    d, n, cls, method, K, inst = CONFIGS[args.config]
+    ctx = tkamd.Context(local_rank)
+    part = tkamd.Partition(d, world, rank)
+    if world > 1:
+        import torch
+        uid = bytearray(tkamd.unique_id()) if rank == 0 else bytearray(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        ctx.init_comm(bytes(t.tolist()), world, rank)
+
+    csc = tkamd.assemble_matrix(n, cls)
+    nnz = int(csc[0][-1])
+    A = tkamd.DeviceMatrix(ctx, csc)
+    bs = []
+    for s in part.local():
+        b = np.random.default_rng(1000 + s).random(n)
+        bs.append(b / np.linalg.norm(b))
+    dev = tkamd.DeviceDecomposition(ctx, L.TK_ARNOLDI if method == "TensorArnoldi" else L.TK_LANCZOS,
+                                    d, part.first, [A] * part.nf, bs, K)
+    # exp-sum rank at k = K (Laplace: kappa independent of n and d)
+    sym = inst == "SymInstance"
+    if sym and cls == "Laplace":
+        spec = tkamd.SpectralData(tkamd.KroneckerMatrix(inst, [csc] * d, cls), K)
+        for _ in range(K - 1):
+            spec.update(d)
+        apx = tkamd.ApproximationData(1e-9, True)
+        apx.update(spec)
+        t_rank = len(apx.omega)
+    else:
+        t_rank = 17 if sym else 3
+    rng = np.random.default_rng(7)
+    Ys = [rng.standard_normal((K, t_rank)) for _ in range(part.nf)]
+
+    def sweep():
+        dev.init(False)
+        dev.sweep(0, K)
+        dev.flush(False)
+        dev.basis_mul(K, Ys, want=False)
+
+    def barrier():
+        ctx.sync()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        sweep()
+    barrier()
+    ctx.timing(1)                    # per-step HIP events on the library's stream
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sweep()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    step_ms, step_cnt = ctx.timing_read(L.T_STEP)
+    vy_ms, vy_cnt = ctx.timing_read(L.T_VY)
+    if dist is not None:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+
+    # per-kernel breakdown (separate, untimed pass with per-kernel events)
+    ctx.timing(2)
+    sweep()
+    ctx.sync()
+    kern = {}
+    for name, cls_id in (("pass1_spmv_cgs", L.T_PASS1), ("pass2_cgs", L.T_PASS2), ("finalize", L.T_FIN),
+                         ("reduce_post", L.T_RED), ("basis_mul", L.T_VY), ("exchange", L.T_XCH)):
+        ms, cnt = ctx.timing_read(cls_id)
+        kern[name] = {"avg_us": round(1e3 * ms / cnt, 3) if cnt else None, "launches": cnt}
+    ctx.timing(0)
+
+    iters = K * args.steps
+    value = iters / elapsed
+    # roofline of the Arnoldi step (SpMV + MGS2 + reductions), device time from events
+    alg_step = sum(alg_bytes_step(n, nnz, k) for k in range(1, K + 1)) * part.nf
+    step_avg_s = (step_ms / 1e3) / max(step_cnt, 1)
+    achieved = (alg_step / K) / step_avg_s / 1e9 if step_cnt else None
+    vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
+    vy_flops = 2 * n * K * t_rank * part.nf
+    vy_s = (vy_ms / 1e3) / max(vy_cnt, 1)
+
+    out = None
+    if rank == 0:
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
+        if os.path.exists(pmc_path):
+            try:
+                traffic = json.load(open(pmc_path)).get("hbm_bytes_per_step")
+            except Exception:
+                traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(csc, n, d, K, args.cpu_seconds)
+        out = {
+            "metric": "Krylov iterations/sec (d-dim Laplacian tensor Krylov, SpMV+MGS2 per factor)",
+            "value": round(value, 3),
+            "unit": "iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (assemble_matrix Laplace; b_s ~ U(0,1) seed 1000+s, normalized)",
+            "config": {"workload": "%s: d=%d n_s=%d %s %s K=%d, factors over %d GPU(s); "
+                                   "step = 1 sweep of K iterations + V*Y (t=%d)"
+                                   % (args.config, d, n, cls, method, K, world, t_rank),
+                       "d": d, "n_s": n, "nmax": K, "matrix": cls, "method": method,
+                       "parallelism": "factor-partition x%d (RCCL all-reduce of records per iteration)" % world},
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors",
+                "achieved": round(achieved, 1) if achieved else None,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg_step / K,
+                "avg_launch_us": round(step_avg_s * 1e6, 2),
+            },
+            "basis_mul_mfma": {
+                "avg_us": round(vy_s * 1e6, 2),
+                "GB_s": round(vy_bytes / vy_s / 1e9, 1) if vy_cnt else None,
+                "TFLOP_s": round(vy_flops / vy_s / 1e12, 3) if vy_cnt else None,
+                "mfma_fp64_peak_TF": FP64_MFMA_PEAK_TF,
+            },
+            "kernels": kern,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    dev.close()
+    A.close()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(csc, n, d, K, seconds):
+    """The oracle's per-factor Arnoldi step timed on the host, on a bounded sample:
+    one factor of the same workload, steps k = 1, 2, ... until `seconds` elapse; the
+    per-k times are extrapolated (linear in k) to the K-step sweep of all d factors."""
+    try:
+        sys.path.insert(0, ROOT)
+        from oracle import tk_ref
+        return tk_ref.baseline(csc, n, d, K, seconds)
+    except Exception as e:   # noqa: BLE001
+        return {"value": None, "unit": "iterations/s", "cores": None, "kind": "port",
+                "sample": "unavailable: %s" % e}
+
+
+if __name__ == "__main__":
+    main()

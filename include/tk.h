@@ -1,0 +1,170 @@
+/*
+ * tk.h -- C ABI of libtkhip.so, the MI355X (gfx950) implementation of the inner Krylov
+ * iteration of thbake/TensorKrylov.jl (tensorkrylov!, src/tensor_krylov_method.jl:36-125).
+ *
+ * The library owns every device buffer; callers pass plain host pointers and sizes.
+ * No call retains a host pointer after it returns.  Every entry point returns a
+ * tk_status (0 = TK_OK); on failure tk_last_error() (thread-local) says why.  Nothing
+ * throws or aborts across this boundary.  A tk_ctx is externally synchronised (one
+ * host thread at a time), exactly like the reference's single-threaded Julia driver.
+ *
+ * Conventions
+ *   - fp64 throughout (the reference is Float64 everywhere).
+ *   - Column index j of a Krylov basis is 0-based: reference step k (1-based,
+ *     orthonormalize!(decomp, k, ...)) is ABI step j = k - 1; it consumes V[:, j] and
+ *     produces H[0..j+1, j] and V[:, j+1].
+ *   - Sparse inputs are Julia's SparseMatrixCSC{Float64,Int64} fields; one_based = 1
+ *     accepts them unmodified (Julia's 1-based colptr/rowval).
+ *   - One process per GPU: a tk_ctx binds one HIP device and one stream.  When the d
+ *     factors are partitioned over ranks, each rank creates its decomposition with its
+ *     own contiguous block of factors and the per-step records are summed over ranks
+ *     with one RCCL all-reduce (tk_comm_init).
+ *
+ * Reference interfaces each entry point replaces are cited per declaration
+ * (paths relative to the reference repository root).
+ */
+#ifndef TK_H_
+#define TK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int tk_status;
+enum {
+    TK_OK = 0,
+    TK_ERR_ARG = 1,      /* invalid argument / shape                          */
+    TK_ERR_HIP = 2,      /* HIP runtime error (message carries hipGetErrorString) */
+    TK_ERR_ALLOC = 3,    /* device or host allocation failed                  */
+    TK_ERR_STATE = 4,    /* call out of sequence (e.g. step j != next step)   */
+    TK_ERR_RCCL = 5,     /* RCCL error                                         */
+    TK_ERR_NODEV = 6     /* no usable gfx950 device                            */
+};
+
+/* Orthonormalization types: src/decompositions.jl:120-176 (TensorArnoldi,
+ * TensorLanczos, TensorLanczosReorth) dispatched by get_orthogonalization,
+ * src/orthogonal_bases.jl:11-13. */
+enum {
+    TK_ARNOLDI = 0,          /* MGS, src/orthogonal_bases.jl:15-37   */
+    TK_LANCZOS = 1,          /* TTR, src/orthogonal_bases.jl:39-67   */
+    TK_LANCZOS_REORTH = 2    /* TTR + loss check + MGS redo, :98-139 */
+};
+
+typedef struct tk_ctx tk_ctx;
+typedef struct tk_mat tk_mat;
+typedef struct tk_decomp tk_decomp;
+
+/* ---------------------------------------------------------------- library / context */
+const char* tk_last_error(void);
+int tk_version(void);                         /* 100 * major + minor */
+/* Bind `device` (HIP ordinal) and create the context's stream. */
+tk_status tk_ctx_create(int device, tk_ctx** out);
+tk_status tk_ctx_destroy(tk_ctx* ctx);
+tk_status tk_ctx_sync(tk_ctx* ctx);
+
+/* ---------------------------------------------------------------- multi-GPU (RCCL) */
+/* 128-byte RCCL unique id; rank 0 creates it and the host broadcasts it. */
+tk_status tk_comm_unique_id(char id_out[128]);
+/* Join an nranks-wide communicator on ctx's device.  Replaces nothing in the
+ * reference (which is single process); it carries the one per-iteration exchange of
+ * the compressed quantities. */
+tk_status tk_comm_init(tk_ctx* ctx, const char id[128], int nranks, int rank);
+/* In-place sum all-reduce of `count` doubles of host memory through the device (test
+ * and control-plane use; the hot path's exchange is internal to tk_decomp_step). */
+tk_status tk_comm_allreduce_host(tk_ctx* ctx, double* buf, size_t count);
+
+/* ---------------------------------------------------------------- coefficient matrices */
+/* A_s as SparseMatrixCSC (src/tensor_struct.jl:48-68 assemble_matrix, stored in
+ * KroneckerMatrix, :168-231).  Converted to device CSR (row-major, ascending column
+ * within a row, int32 indices) so that each row sum y[i] = sum_p val[p]*x[col[p]]
+ * adds terms in the order of Julia's CSC scatter mul! (no FMA): results equal the
+ * reference SpMV bit for bit. */
+tk_status tk_matrix_from_csc(tk_ctx* ctx, int64_t n, const int64_t* colptr,
+                             const int64_t* rowval, const double* nzval,
+                             int one_based, tk_mat** out);
+tk_status tk_matrix_from_csr(tk_ctx* ctx, int64_t n, const int64_t* rowptr,
+                             const int64_t* colind, const double* val,
+                             int one_based, tk_mat** out);
+tk_status tk_matrix_destroy(tk_mat* A);
+/* y = A x on the device (host in/out buffers; test hook for mul!, used at
+ * src/orthogonal_bases.jl:20,45,103). */
+tk_status tk_matvec(tk_mat* A, const double* x, double* y);
+
+/* ---------------------------------------------------------------- tensor decomposition */
+/* Create the state of this rank's factors s = first_factor .. first_factor+nf-1 of a
+ * d_total-factor decomposition (TensorArnoldi(A) / TensorLanczos(A) /
+ * TensorLanczosReorth(A), src/decompositions.jl:127-174; storage capped at kmax+1
+ * basis columns instead of n+1).  mats[i], b[i] (length n, host) are factor
+ * first_factor+i's A_s and b_s.  All factors share n (src/tensor_krylov_method.jl:46).
+ * kmax = nmax; steps j = 0 .. kmax-1 are allowed.
+ * track_all_gram != 0 keeps the Gram row of every factor (always on for
+ * TK_LANCZOS_REORTH); otherwise only global factor 0's (for the driver's
+ * orthogonality_data, src/tensor_krylov_method.jl:103). */
+tk_status tk_decomp_create(tk_ctx* ctx, int method, int d_total, int first_factor, int nf,
+                           tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
+                           int track_all_gram, tk_decomp** out);
+tk_status tk_decomp_destroy(tk_decomp* dc);
+
+/* Per-factor record layout (doubles; m = tk_record_len(kmax)), written by every step:
+ *   [0 .. kmax+1]        H[0..j+1, j] as computed by this step (rest 0)
+ *   [kmax+2 .. 2kmax+3]  Gram row G[c, 0..c] = V[:,c]' V[:,0..c] of column c below
+ *   [2kmax+4]            btilde[c] = <V[:,c], b_s>   (update_rhs!, src/utils.jl:466-476)
+ *   [2kmax+5]            c (column of the Gram row / btilde entry), -1 if none
+ *   [2kmax+6]            beta = H[j+1, j] (after any re-orthogonalization)
+ *   [2kmax+7]            loss (LanczosReorth: ||V[:,0..j+1]'V[:,0..j+1] - I||_F after TTR)
+ *   [2kmax+8]            1.0 if LanczosReorth re-orthogonalized this step (MGS redo)
+ *   [2kmax+9]            Gram tracked for this factor (1.0) or not (0.0)
+ * Records are laid out [d_total][m]; slots of factors owned by other ranks are summed
+ * in by the all-reduce (zero otherwise). */
+int tk_record_len(int kmax);
+
+/* initialize_decomp! + initialize_compressed_rhs (src/decompositions.jl:112-118,
+ * src/utils.jl:456-464): V[:,0] = inv(norm(b)) .* b; record carries btilde[0] and
+ * G[0,0].  rec_out: [d_total][m] or NULL (then nothing is synchronised). */
+tk_status tk_decomp_init(tk_decomp* dc, double* rec_out);
+
+/* orthonormalize!(td, k) for all of this rank's factors, k = j+1
+ * (src/orthogonal_bases.jl:142-180 fan-out; per-factor steps :15-37 / :39-67 /
+ * :98-139).  Must be called with j = 0, 1, ... in order.  The record of step j holds
+ * H[0..j+1, j] and, for the fused pipeline, btilde[j] and G[j, 0..j] of column j.
+ * rec_out NULL = asynchronous (records stay on the device; see tk_decomp_records). */
+tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out);
+
+/* Enqueue steps j0 .. j1-1 back to back with no host synchronisation (the device
+ * iteration of the driver loop, src/tensor_krylov_method.jl:63-66).  Not valid for
+ * TK_LANCZOS_REORTH (its loss check is a host decision per step). */
+tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1);
+
+/* Write the last pending basis column V[:, j+1] (the fused pipeline defers it into
+ * the next step); its btilde / Gram row go to the flush record.  rec_out may be NULL. */
+tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out);
+
+/* Copy records of slots s0 .. s1-1 (slot 0 = init, slot j+1 = step j,
+ * slot kmax+1 = last flush) to host out[(s1-s0)][d_total][m]. */
+tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out);
+
+/* Copy V[:, c0 .. c0+nc-1] of local factor f (0-based within this rank) to host
+ * (column-major n x nc).  Flushes a pending column first. */
+tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out);
+
+/* basis_tensor_mul! (src/utils.jl:478-488, called at src/tensor_krylov_method.jl:112):
+ * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).
+ * Y: host [nf][t][k] (each Y_s column-major k x t).  X: host [nf][t][n] (column-major
+ * n x t each) or NULL to leave the product on the device (benchmarks).
+ * Flushes a pending column first. */
+tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X);
+
+/* ---------------------------------------------------------------- timing hooks */
+/* Average device time (ms) per launch of the named kernel class recorded with HIP
+ * events on the ctx stream since the last reset; classes: 0 = all step kernels,
+ * 1 = the dominant streaming kernel (Arnoldi/Lanczos projection), 2 = basis_mul. */
+tk_status tk_timing_enable(tk_ctx* ctx, int on);
+tk_status tk_timing_read(tk_ctx* ctx, int cls, double* total_ms, long* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TK_H_ */

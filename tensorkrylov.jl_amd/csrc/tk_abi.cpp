@@ -1,0 +1,762 @@
+// tk_abi.cpp -- C ABI of libtkhip.so (include/tk.h): device state ownership, step
+// sequencing (the per-factor fan-out of src/orthogonal_bases.jl:142-180 as ONE batched
+// launch set over all of this rank's factors), the one RCCL all-reduce per step, and
+// HIP-event timing.  No host pointer is retained after a call returns.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/tk.h"
+#include "tk_internal.h"
+
+using namespace tk;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static tk_status fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) return fail(TK_ERR_HIP, "%s: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+#define LAUNCHCHK(what)                                                                   \
+    do {                                                                                  \
+        hipError_t e_ = hipGetLastError();                                                \
+        if (e_ != hipSuccess) return fail(TK_ERR_HIP, "launch %s: %s", what, hipGetErrorString(e_)); \
+    } while (0)
+#define NCCLCHK(x)                                                                        \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess) return fail(TK_ERR_RCCL, "%s: %s", #x, ncclGetErrorString(r_)); \
+    } while (0)
+#define CHECKARG(c, msg)                      \
+    do {                                      \
+        if (!(c)) return fail(TK_ERR_ARG, "%s", msg); \
+    } while (0)
+
+// ------------------------------------------------------------------ context
+enum { TCLS_STEP = 0, TCLS_PASS1 = 1, TCLS_PASS2 = 2, TCLS_FIN = 3, TCLS_RED = 4, TCLS_VY = 5, TCLS_XCH = 6, TCLS_N = 8 };
+
+struct tk_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    int timing = 0;   // 0 off, 1 step level, 2 per kernel class
+    std::vector<hipEvent_t> ev[TCLS_N];   // start/stop pairs
+    double ms[TCLS_N] = {0};
+    long cnt[TCLS_N] = {0};
+    double* xbuf = nullptr;   // host-allreduce staging
+    size_t xcap = 0;
+};
+
+struct Timer {
+    tk_ctx* c;
+    int cls;
+    bool on;
+    hipEvent_t b = nullptr;
+    Timer(tk_ctx* c_, int cls_, int level) : c(c_), cls(cls_), on(c_->timing >= level) {
+        if (!on) return;
+        hipEvent_t a;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
+        hipEventRecord(a, c->stream);
+        c->ev[cls].push_back(a);
+    }
+    ~Timer() {
+        if (!on) return;
+        hipEventRecord(b, c->stream);
+        c->ev[cls].push_back(b);
+    }
+};
+
+static void drain_timers(tk_ctx* c) {
+    for (int k = 0; k < TCLS_N; ++k) {
+        auto& v = c->ev[k];
+        if (v.empty()) continue;
+        hipEventSynchronize(v.back());
+        for (size_t i = 0; i + 1 < v.size(); i += 2) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, v[i], v[i + 1]) == hipSuccess) {
+                c->ms[k] += ms;
+                c->cnt[k] += 1;
+            }
+            hipEventDestroy(v[i]);
+            hipEventDestroy(v[i + 1]);
+        }
+        v.clear();
+    }
+}
+
+extern "C" {
+
+const char* tk_last_error(void) { return g_err.c_str(); }
+int tk_version(void) { return 100; }
+
+tk_status tk_ctx_create(int device, tk_ctx** out) {
+    CHECKARG(out, "out is NULL");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TK_ERR_NODEV, "no HIP device visible");
+    CHECKARG(device >= 0 && device < ndev, "device ordinal out of range");
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(TK_ERR_NODEV, "device %d is %s; libtkhip is built for gfx950 only", device, prop.gcnArchName);
+    tk_ctx* c = new tk_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(TK_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    *out = c;
+    return TK_OK;
+}
+
+tk_status tk_ctx_destroy(tk_ctx* c) {
+    if (!c) return TK_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    drain_timers(c);
+    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->xbuf) hipFree(c->xbuf);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return TK_OK;
+}
+
+tk_status tk_ctx_sync(tk_ctx* c) {
+    CHECKARG(c, "ctx is NULL");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TK_OK;
+}
+
+tk_status tk_comm_unique_id(char id_out[128]) {
+    CHECKARG(id_out, "id_out is NULL");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+    memcpy(id_out, &id, 128);
+    return TK_OK;
+}
+
+tk_status tk_comm_init(tk_ctx* c, const char id[128], int nranks, int rank) {
+    CHECKARG(c && id, "NULL argument");
+    CHECKARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad nranks/rank");
+    HIPCHK(hipSetDevice(c->device));
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return TK_OK;
+}
+
+tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) {
+    CHECKARG(c && buf, "NULL argument");
+    if (!c->comm || c->nranks == 1) return TK_OK;
+    HIPCHK(hipSetDevice(c->device));
+    if (count > c->xcap) {
+        if (c->xbuf) hipFree(c->xbuf);
+        c->xbuf = nullptr;
+        HIPCHK(hipMalloc(&c->xbuf, count * sizeof(double)));
+        c->xcap = count;
+    }
+    HIPCHK(hipMemcpyAsync(c->xbuf, buf, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    NCCLCHK(ncclAllReduce(c->xbuf, c->xbuf, count, ncclDouble, ncclSum, c->comm, c->stream));
+    HIPCHK(hipMemcpyAsync(buf, c->xbuf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return TK_OK;
+}
+
+// ------------------------------------------------------------------ matrices
+struct tk_mat {
+    tk_ctx* ctx;
+    int64_t n = 0, nnz = 0;
+    int* rowptr = nullptr;
+    int* col = nullptr;
+    double* val = nullptr;
+};
+
+static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
+                            const std::vector<double>& v, tk_mat** out) {
+    tk_mat* A = new tk_mat();
+    A->ctx = c;
+    A->n = n;
+    A->nnz = (int64_t)ci.size();
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMalloc(&A->rowptr, (n + 1) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&A->col, std::max<int64_t>(A->nnz, 1) * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc(&A->val, std::max<int64_t>(A->nnz, 1) * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(A->rowptr, rp.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess && A->nnz) e = hipMemcpy(A->col, ci.data(), A->nnz * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess && A->nnz) e = hipMemcpy(A->val, v.data(), A->nnz * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        hipFree(A->rowptr);
+        hipFree(A->col);
+        hipFree(A->val);
+        delete A;
+        return fail(TK_ERR_ALLOC, "matrix upload: %s", hipGetErrorString(e));
+    }
+    *out = A;
+    return TK_OK;
+}
+
+tk_status tk_matrix_from_csc(tk_ctx* c, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                             const double* nzval, int one_based, tk_mat** out) {
+    CHECKARG(c && colptr && out && n > 0, "bad argument");
+    const int64_t base = one_based ? 1 : 0;
+    const int64_t nnz = colptr[n] - colptr[0];
+    CHECKARG(nnz >= 0 && nnz < (int64_t)INT32_MAX, "nnz out of range");
+    CHECKARG(nnz == 0 || (rowval && nzval), "rowval/nzval NULL");
+    // CSC -> CSR: scanning columns in ascending order leaves every row's entries in
+    // ascending column order, i.e. the order Julia's scatter mul! adds them.
+    std::vector<int> rp(n + 1, 0), ci(nnz);
+    std::vector<double> v(nnz);
+    for (int64_t p = 0; p < nnz; ++p) {
+        const int64_t r = rowval[p] - base;
+        if (r < 0 || r >= n) return fail(TK_ERR_ARG, "row index %lld out of range", (long long)rowval[p]);
+        rp[r + 1]++;
+    }
+    for (int64_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+    std::vector<int> fill(rp.begin(), rp.end() - 1);
+    for (int64_t j = 0; j < n; ++j) {
+        const int64_t p0 = colptr[j] - colptr[0], p1 = colptr[j + 1] - colptr[0];
+        if (p1 < p0) return fail(TK_ERR_ARG, "colptr not monotone at %lld", (long long)j);
+        for (int64_t p = p0; p < p1; ++p) {
+            const int64_t r = rowval[p] - base;
+            const int q = fill[r]++;
+            ci[q] = (int)j;
+            v[q] = nzval[p];
+        }
+    }
+    return upload_csr(c, n, rp, ci, v, out);
+}
+
+tk_status tk_matrix_from_csr(tk_ctx* c, int64_t n, const int64_t* rowptr, const int64_t* colind,
+                             const double* val, int one_based, tk_mat** out) {
+    CHECKARG(c && rowptr && out && n > 0, "bad argument");
+    const int64_t base = one_based ? 1 : 0;
+    const int64_t nnz = rowptr[n] - rowptr[0];
+    CHECKARG(nnz >= 0 && nnz < (int64_t)INT32_MAX, "nnz out of range");
+    std::vector<int> rp(n + 1), ci(nnz);
+    std::vector<double> v(nnz);
+    for (int64_t i = 0; i <= n; ++i) rp[i] = (int)(rowptr[i] - rowptr[0]);
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t last = -1;
+        for (int64_t p = rp[i]; p < rp[i + 1]; ++p) {
+            const int64_t cc = colind[p] - base;
+            if (cc < 0 || cc >= n) return fail(TK_ERR_ARG, "column index out of range in row %lld", (long long)i);
+            if (cc <= last) return fail(TK_ERR_ARG, "row %lld: columns not strictly ascending", (long long)i);
+            last = cc;
+            ci[p] = (int)cc;
+            v[p] = val[p];
+        }
+    }
+    return upload_csr(c, n, rp, ci, v, out);
+}
+
+tk_status tk_matrix_destroy(tk_mat* A) {
+    if (!A) return TK_OK;
+    hipSetDevice(A->ctx->device);
+    hipFree(A->rowptr);
+    hipFree(A->col);
+    hipFree(A->val);
+    delete A;
+    return TK_OK;
+}
+
+tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
+    CHECKARG(A && x && y, "NULL argument");
+    tk_ctx* c = A->ctx;
+    HIPCHK(hipSetDevice(c->device));
+    double *dx = nullptr, *dy = nullptr;
+    HIPCHK(hipMalloc(&dx, A->n * sizeof(double)));
+    hipError_t e = hipMalloc(&dy, A->n * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpyAsync(dx, x, A->n * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        launch_spmv(A->rowptr, A->col, A->val, dx, dy, A->n, c->stream);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(y, dy, A->n * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    hipFree(dx);
+    hipFree(dy);
+    if (e != hipSuccess) return fail(TK_ERR_HIP, "tk_matvec: %s", hipGetErrorString(e));
+    return TK_OK;
+}
+
+// ------------------------------------------------------------------ decomposition
+struct tk_decomp {
+    tk_ctx* ctx;
+    int method, d_total, foff, nf, kmax, m, nvmax;
+    int64_t n, ld;
+    int ntiles, npart;
+    int jnext = 0;          // next step index
+    bool inited = false;
+    bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
+    int last_j = -1;
+    std::vector<tk_mat*> mats;
+    std::vector<DFac> hf;   // host copy of descriptors
+    DFac* df = nullptr;     // device descriptors
+    std::vector<void*> allocs;
+    double* rec = nullptr;  // [(kmax+2) slots][d_total][m]
+    double* Ydev = nullptr; size_t ycap = 0;
+    double* Xdev = nullptr; size_t xcap = 0;
+    // host Gram mirror (LanczosReorth decisions): [nf][(kmax+1)^2]
+    std::vector<std::vector<double>> gram;
+};
+
+int tk_record_len(int kmax) { return rec_len(kmax); }
+
+static tk_status dalloc(tk_decomp* dc, void** p, size_t bytes) {
+    hipError_t e = hipMalloc(p, std::max<size_t>(bytes, 16));
+    if (e != hipSuccess) return fail(TK_ERR_ALLOC, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    dc->allocs.push_back(*p);
+    e = hipMemset(*p, 0, std::max<size_t>(bytes, 16));
+    if (e != hipSuccess) return fail(TK_ERR_HIP, "hipMemset: %s", hipGetErrorString(e));
+    return TK_OK;
+}
+
+static void free_decomp(tk_decomp* dc) {
+    for (void* p : dc->allocs) hipFree(p);
+    delete dc;
+}
+
+tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,
+                           tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
+                           int track_all_gram, tk_decomp** out) {
+    CHECKARG(c && mats && b && out, "NULL argument");
+    CHECKARG(method >= TK_ARNOLDI && method <= TK_LANCZOS_REORTH, "unknown method");
+    CHECKARG(nf >= 1 && d_total >= 1 && first_factor >= 0 && first_factor + nf <= d_total, "bad factor range");
+    CHECKARG(kmax >= 1 && kmax <= 1000, "kmax out of range [1, 1000]");
+    CHECKARG(n >= 1, "n must be positive");
+    for (int f = 0; f < nf; ++f) {
+        CHECKARG(mats[f] && b[f], "NULL matrix or rhs");
+        if (mats[f]->n != n) return fail(TK_ERR_ARG, "factor %d has order %lld != n = %lld", f, (long long)mats[f]->n, (long long)n);
+        if (mats[f]->ctx != c) return fail(TK_ERR_ARG, "factor %d matrix belongs to another context", f);
+    }
+    HIPCHK(hipSetDevice(c->device));
+    tk_decomp* dc = new tk_decomp();
+    dc->ctx = c;
+    dc->method = method;
+    dc->d_total = d_total;
+    dc->foff = first_factor;
+    dc->nf = nf;
+    dc->kmax = kmax;
+    dc->m = rec_len(kmax);
+    dc->n = n;
+    dc->ld = (n + 255) / 256 * 256;
+    dc->ntiles = (int)((n + 255) / 256);
+    dc->npart = std::min(dc->ntiles, 1024);
+    dc->nvmax = 2 * kmax + 8;
+    dc->mats.assign(mats, mats + nf);
+    dc->hf.resize(nf);
+    const int KP = kmax + 2, KC = kmax + 1;
+    tk_status st = TK_OK;
+#define DA(ptr, bytes)                                          \
+    do {                                                        \
+        void* p_ = nullptr;                                     \
+        st = dalloc(dc, &p_, (bytes));                          \
+        if (st != TK_OK) { free_decomp(dc); return st; }        \
+        ptr = (decltype(ptr))p_;                                \
+    } while (0)
+    for (int f = 0; f < nf; ++f) {
+        DFac& d = dc->hf[f];
+        d.rowptr = mats[f]->rowptr;
+        d.col = mats[f]->col;
+        d.val = mats[f]->val;
+        DA(d.V, (size_t)dc->ld * KC * sizeof(double));
+        double* bb;
+        DA(bb, (size_t)dc->ld * sizeof(double));
+        hipError_t e = hipMemcpy(bb, b[f], n * sizeof(double), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload b: %s", hipGetErrorString(e)); }
+        d.b = bb;
+        DA(d.W, (size_t)dc->ld * sizeof(double));
+        DA(d.U, (size_t)dc->ld * sizeof(double));
+        DA(d.P1, (size_t)dc->nvmax * dc->npart * sizeof(double));
+        DA(d.P2, (size_t)dc->nvmax * dc->npart * sizeof(double));
+        DA(d.RED1, (size_t)dc->nvmax * sizeof(double));
+        DA(d.RED2, (size_t)dc->nvmax * sizeof(double));
+        DA(d.sc, SC_COUNT * sizeof(double));
+        DA(d.h2, KP * sizeof(double));
+        DA(d.g, KP * sizeof(double));
+        DA(d.H, (size_t)KP * KC * sizeof(double));
+        const int gi = first_factor + f;
+        d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
+        d.gidx = gi;
+    }
+    DA(dc->df, nf * sizeof(DFac));
+    {
+        hipError_t e = hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice);
+        if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
+    }
+    DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+#undef DA
+    if (method == TK_LANCZOS_REORTH) dc->gram.assign(nf, std::vector<double>((size_t)KC * KC, 0.0));
+    *out = dc;
+    return TK_OK;
+}
+
+tk_status tk_decomp_destroy(tk_decomp* dc) {
+    if (!dc) return TK_OK;
+    hipSetDevice(dc->ctx->device);
+    hipStreamSynchronize(dc->ctx->stream);
+    free_decomp(dc);
+    return TK_OK;
+}
+
+static KArgs base_args(tk_decomp* dc, int j, int slot) {
+    KArgs a;
+    a.n = dc->n;
+    a.ld = dc->ld;
+    a.j = j;
+    a.npart = dc->npart;
+    a.ntiles = dc->ntiles;
+    a.kmax = dc->kmax;
+    a.m = dc->m;
+    a.rec = dc->rec + (size_t)slot * dc->d_total * dc->m;
+    return a;
+}
+
+static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out) {
+    tk_ctx* c = dc->ctx;
+    double* s = dc->rec + (size_t)slot * dc->d_total * dc->m;
+    const size_t cnt = (size_t)dc->d_total * dc->m;
+    if (c->comm && c->nranks > 1) {
+        Timer tm(c, TCLS_XCH, 2);
+        NCCLCHK(ncclAllReduce(s, s, cnt, ncclDouble, ncclSum, c->comm, c->stream));
+    }
+    if (rec_out) {
+        HIPCHK(hipMemcpyAsync(rec_out, s, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return TK_OK;
+}
+
+static tk_status clear_slot(tk_decomp* dc, int slot) {
+    double* s = dc->rec + (size_t)slot * dc->d_total * dc->m;
+    HIPCHK(hipMemsetAsync(s, 0, (size_t)dc->d_total * dc->m * sizeof(double), dc->ctx->stream));
+    return TK_OK;
+}
+
+#define RUN(cls, level, call, name)        \
+    do {                                   \
+        Timer tm_(c, cls, level);          \
+        call;                              \
+    } while (0);                           \
+    LAUNCHCHK(name)
+
+tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
+    CHECKARG(dc, "NULL decomp");
+    tk_ctx* c = dc->ctx;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    tk_status st = clear_slot(dc, 0);
+    if (st) return st;
+    KArgs a = base_args(dc, 0, 0);
+    const int nf = dc->nf;
+    RUN(TCLS_PASS1, 2, launch_init_a(dc->df, nf, a, s), "init_a");
+    RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
+    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_A, 0, s), "post");
+    RUN(TCLS_PASS1, 2, launch_init_b(dc->df, nf, a, s), "init_b");
+    RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2, dc->npart, s), "reduce");
+    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, s), "post");
+    dc->inited = true;
+    dc->jnext = 0;
+    dc->pending = false;
+    dc->last_j = -1;
+    if (dc->method == TK_LANCZOS_REORTH) {
+        // G[0,0] for the host loss mirror
+        std::vector<double> r((size_t)dc->d_total * dc->m);
+        st = exchange_and_copy(dc, 0, r.data());
+        if (st) return st;
+        for (int f = 0; f < nf; ++f)
+            dc->gram[f][0] = r[(size_t)(dc->foff + f) * dc->m + rec_gram(dc->kmax)];
+        if (rec_out) memcpy(rec_out, r.data(), r.size() * sizeof(double));
+        return TK_OK;
+    }
+    return exchange_and_copy(dc, 0, rec_out);
+}
+
+// write the pending column (Arnoldi / Lanczos fused pipeline)
+static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
+    tk_ctx* c = dc->ctx;
+    hipStream_t s = c->stream;
+    const int nf = dc->nf, j = a.j;
+    if (dc->method == TK_ARNOLDI) {
+        RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, a, s), "arn_finalize");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, s), "post");
+    } else {
+        RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, s), "post");
+    }
+    return TK_OK;
+}
+
+static double gram_loss(const std::vector<double>& G, int KC, int ncols) {
+    // ||G[0..ncols) - I||_F with G symmetric, rows stored as G[c*KC + i], i <= c
+    double s = 0.0;
+    for (int cidx = 0; cidx < ncols; ++cidx)
+        for (int i = 0; i <= cidx; ++i) {
+            const double v = G[(size_t)cidx * KC + i] - (i == cidx ? 1.0 : 0.0);
+            s += (i == cidx ? 1.0 : 2.0) * v * v;
+        }
+    return sqrt(s);
+}
+
+static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
+    tk_ctx* c = dc->ctx;
+    hipStream_t s = c->stream;
+    const int nf = dc->nf, slot = j + 1;
+    tk_status st = clear_slot(dc, slot);
+    if (st) return st;
+    KArgs a = base_args(dc, j, slot);
+    Timer step_timer(c, TCLS_STEP, 1);
+    if (dc->method == TK_ARNOLDI) {
+        const bool fused = dc->pending;
+        if (fused) {
+            RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2 * j + 3, dc->npart, s), "reduce");
+        } else {
+            RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
+        }
+        RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, j + 2, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, s), "post");
+        dc->pending = true;
+    } else if (dc->method == TK_LANCZOS) {
+        const bool fused = dc->pending;
+        if (fused) {
+            RUN(TCLS_PASS1, 2, launch_lan_l1_fused(dc->df, nf, a, s), "lan_l1_fused");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        } else {
+            RUN(TCLS_PASS1, 2, launch_lan_l1_plain(dc->df, nf, a, s), "lan_l1_plain");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
+        }
+        RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, fused ? 1 : 0, s), "post");
+        dc->pending = true;
+    } else {
+        // TensorLanczosReorth (src/orthogonal_bases.jl:98-139): TTR, write v_{j+1},
+        // host loss check, MGS redo of step j for the factors that need it.
+        RUN(TCLS_PASS1, 2, launch_lan_l1_plain(dc->df, nf, a, s), "lan_l1_plain");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
+        RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, 0, s), "post");
+        RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, s), "post");
+        const size_t cnt = (size_t)dc->d_total * dc->m;
+        std::vector<double> r(cnt);
+        double* slotp = a.rec;
+        HIPCHK(hipMemcpyAsync(r.data(), slotp, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const int KC = dc->kmax + 1, kmax = dc->kmax, m = dc->m;
+        const double thr = sqrt(2.220446049250313e-16);
+        std::vector<int> redo(nf, 0);
+        std::vector<double> loss(nf, 0.0);
+        bool any = false;
+        for (int f = 0; f < nf; ++f) {
+            const double* rf = r.data() + (size_t)(dc->foff + f) * m;
+            for (int i = 0; i <= j + 1; ++i) dc->gram[f][(size_t)(j + 1) * KC + i] = rf[rec_gram(kmax) + i];
+            loss[f] = gram_loss(dc->gram[f], KC, j + 2);
+            redo[f] = loss[f] > thr;
+            any = any || redo[f];
+        }
+        if (any) {
+            // Redo step j with MGS for the selected factors: run the Arnoldi kernels on a
+            // descriptor array that contains only those factors.
+            std::vector<DFac> sub;
+            for (int f = 0; f < nf; ++f)
+                if (redo[f]) sub.push_back(dc->hf[f]);
+            DFac* dsub = nullptr;
+            HIPCHK(hipMallocAsync((void**)&dsub, sub.size() * sizeof(DFac), s));
+            HIPCHK(hipMemcpyAsync(dsub, sub.data(), sub.size() * sizeof(DFac), hipMemcpyHostToDevice, s));
+            const int ns = (int)sub.size();
+            RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dsub, ns, a, s), "arn_a1_plain");
+            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 1, dc->npart, s), "reduce");
+            RUN(TCLS_PASS2, 2, launch_arn_a2(dsub, ns, a, s), "arn_a2");
+            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 2, j + 2, dc->npart, s), "reduce");
+            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN, 0, s), "post");
+            RUN(TCLS_FIN, 2, launch_arn_finalize(dsub, ns, a, s), "arn_finalize");
+            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 3, dc->npart, s), "reduce");
+            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN_FIN, 0, s), "post");
+            HIPCHK(hipFreeAsync(dsub, s));
+            HIPCHK(hipMemcpyAsync(r.data(), slotp, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (int f = 0; f < nf; ++f) {
+                if (!redo[f]) continue;
+                const double* rf = r.data() + (size_t)(dc->foff + f) * m;
+                for (int i = 0; i <= j + 1; ++i) dc->gram[f][(size_t)(j + 1) * KC + i] = rf[rec_gram(kmax) + i];
+            }
+        }
+        // loss / flag fields for the local factors
+        for (int f = 0; f < nf; ++f) {
+            double* rf = r.data() + (size_t)(dc->foff + f) * m;
+            rf[rec_loss(kmax)] = loss[f];
+            rf[rec_flag(kmax)] = redo[f] ? 1.0 : 0.0;
+            HIPCHK(hipMemcpyAsync(slotp + (size_t)(dc->foff + f) * m + rec_loss(kmax), rf + rec_loss(kmax),
+                                  2 * sizeof(double), hipMemcpyHostToDevice, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));
+        dc->pending = false;
+    }
+    dc->last_j = j;
+    dc->jnext = j + 1;
+    return TK_OK;
+}
+
+tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
+    CHECKARG(dc, "NULL decomp");
+    if (!dc->inited) return fail(TK_ERR_STATE, "tk_decomp_init not called");
+    if (j != dc->jnext) return fail(TK_ERR_STATE, "step %d requested, next step is %d", j, dc->jnext);
+    if (j >= dc->kmax) return fail(TK_ERR_ARG, "step %d >= kmax %d", j, dc->kmax);
+    HIPCHK(hipSetDevice(dc->ctx->device));
+    tk_status st = step_impl(dc, j, rec_out);
+    if (st) return st;
+    return exchange_and_copy(dc, j + 1, rec_out);
+}
+
+tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
+    CHECKARG(dc, "NULL decomp");
+    if (dc->method == TK_LANCZOS_REORTH) return fail(TK_ERR_ARG, "tk_decomp_sweep: LanczosReorth needs a host decision per step");
+    for (int j = j0; j < j1; ++j) {
+        tk_status st = tk_decomp_step(dc, j, nullptr);
+        if (st) return st;
+    }
+    return TK_OK;
+}
+
+tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {
+    CHECKARG(dc, "NULL decomp");
+    HIPCHK(hipSetDevice(dc->ctx->device));
+    const int slot = dc->kmax + 1;
+    if (!dc->pending) {
+        if (rec_out) {
+            tk_status st = clear_slot(dc, slot);
+            if (st) return st;
+            return exchange_and_copy(dc, slot, rec_out);
+        }
+        return TK_OK;
+    }
+    tk_status st = clear_slot(dc, slot);
+    if (st) return st;
+    KArgs a = base_args(dc, dc->last_j, slot);
+    st = finalize_pending(dc, a);
+    if (st) return st;
+    dc->pending = false;
+    return exchange_and_copy(dc, slot, rec_out);
+}
+
+tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
+    CHECKARG(dc && out, "NULL argument");
+    CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
+    HIPCHK(hipSetDevice(dc->ctx->device));
+    const size_t per = (size_t)dc->d_total * dc->m;
+    HIPCHK(hipMemcpyAsync(out, dc->rec + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
+                          dc->ctx->stream));
+    HIPCHK(hipStreamSynchronize(dc->ctx->stream));
+    return TK_OK;
+}
+
+tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out) {
+    CHECKARG(dc && out, "NULL argument");
+    CHECKARG(f >= 0 && f < dc->nf, "factor out of range");
+    CHECKARG(c0 >= 0 && nc >= 0 && c0 + nc <= dc->kmax + 1, "column range");
+    HIPCHK(hipSetDevice(dc->ctx->device));
+    if (dc->pending && c0 + nc - 1 > dc->last_j) {
+        tk_status st = tk_decomp_flush(dc, nullptr);
+        if (st) return st;
+    }
+    const DFac& d = dc->hf[f];
+    HIPCHK(hipMemcpy2DAsync(out, dc->n * sizeof(double), d.V + (size_t)c0 * dc->ld, dc->ld * sizeof(double),
+                            dc->n * sizeof(double), nc, hipMemcpyDeviceToHost, dc->ctx->stream));
+    HIPCHK(hipStreamSynchronize(dc->ctx->stream));
+    return TK_OK;
+}
+
+tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X) {
+    CHECKARG(dc && Y, "NULL argument");
+    CHECKARG(k >= 1 && k <= dc->kmax + 1 && t >= 1, "bad k/t");
+    tk_ctx* c = dc->ctx;
+    HIPCHK(hipSetDevice(c->device));
+    if (dc->pending && k - 1 > dc->last_j) {
+        tk_status st = tk_decomp_flush(dc, nullptr);
+        if (st) return st;
+    }
+    const size_t ny = (size_t)dc->nf * k * t, nx = (size_t)dc->nf * dc->ld * t;
+    if (ny > dc->ycap) {
+        if (dc->Ydev) hipFree(dc->Ydev);
+        dc->Ydev = nullptr;
+        HIPCHK(hipMalloc(&dc->Ydev, ny * sizeof(double)));
+        dc->ycap = ny;
+    }
+    if (nx > dc->xcap) {
+        if (dc->Xdev) hipFree(dc->Xdev);
+        dc->Xdev = nullptr;
+        HIPCHK(hipMalloc(&dc->Xdev, nx * sizeof(double)));
+        dc->xcap = nx;
+    }
+    hipStream_t s = c->stream;
+    HIPCHK(hipMemcpyAsync(dc->Ydev, Y, ny * sizeof(double), hipMemcpyHostToDevice, s));
+    KArgs a = base_args(dc, 0, 0);
+    RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");
+    if (X) {
+        for (int f = 0; f < dc->nf; ++f)
+            HIPCHK(hipMemcpy2DAsync(X + (size_t)f * dc->n * t, dc->n * sizeof(double),
+                                    dc->Xdev + (size_t)f * dc->ld * t, dc->ld * sizeof(double),
+                                    dc->n * sizeof(double), t, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    return TK_OK;
+}
+
+tk_status tk_timing_enable(tk_ctx* c, int on) {
+    CHECKARG(c, "NULL ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    drain_timers(c);
+    for (int k = 0; k < TCLS_N; ++k) {
+        c->ms[k] = 0.0;
+        c->cnt[k] = 0;
+    }
+    c->timing = on;
+    return TK_OK;
+}
+
+tk_status tk_timing_read(tk_ctx* c, int cls, double* total_ms, long* launches) {
+    CHECKARG(c && total_ms && launches, "NULL argument");
+    CHECKARG(cls >= 0 && cls < TCLS_N, "timing class out of range");
+    HIPCHK(hipSetDevice(c->device));
+    drain_timers(c);
+    *total_ms = c->ms[cls];
+    *launches = c->cnt[cls];
+    return TK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// tk_internal.h -- device-side descriptors shared by tk_kernels.hip and tk_abi.cpp.
+#ifndef TK_INTERNAL_H_
+#define TK_INTERNAL_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tk {
+
+// Scalars kept per factor on the device (DFac::sc).
+enum {
+    SC_BETA = 0,      // beta of the last completed step (H[j+1, j])
+    SC_INVBETA = 1,   // inv(beta)
+    SC_BETAPREV = 2,  // Lanczos beta_{j-1} for a plain (non-fused) TTR step
+    SC_INVB = 3,      // inv(norm(b))
+    SC_BNORM = 4,     // norm(b)
+    SC_COUNT = 8
+};
+
+// Per-factor device descriptor.  One array of these lives in device memory; kernels
+// index it with blockIdx.y, so every launch covers all of this rank's factors.
+struct DFac {
+    const int* rowptr;    // CSR of A_s (n+1)
+    const int* col;       // (nnz) ascending within a row
+    const double* val;    // (nnz)
+    double* V;            // basis, column-major, ld x (kmax+1)
+    const double* b;      // b_s (n)
+    double* W;            // work vector (SpMV output / Lanczos v)
+    double* U;            // work vector (w' / Lanczos u)
+    double* P1;           // block partials [value][npart], first reduction of a step
+    double* P2;           // block partials, second reduction
+    double* RED1;         // reduced values of P1
+    double* RED2;         // reduced values of P2
+    double* sc;           // scalars (SC_*)
+    double* h2;           // second-pass coefficients of the last Arnoldi step (kmax+2)
+    double* g;            // Hbar * h2 (kmax+2)
+    double* H;            // Hessenberg, column-major (kmax+2) x (kmax+1)
+    int track_gram;       // keep Gram rows for this factor
+    int gidx;             // global factor index (record slot)
+};
+
+struct KArgs {
+    int64_t n;        // rows
+    int64_t ld;       // leading dimension of V (n rounded up to 256)
+    int j;            // step (0-based column)
+    int npart;        // partial blocks per factor (function of n only)
+    int ntiles;       // ceil(n / 256)
+    int kmax;
+    int m;            // record length per factor
+    double* rec;      // record slot base ([d_total][m])
+};
+
+// launchers (tk_kernels.hip)
+void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s);
+// post-processing (one 64-thread block per factor)
+enum PostKind {
+    POST_INIT_A = 0,
+    POST_INIT_B = 1,
+    POST_ARN = 2,        // after a2; fused flag in `flag`
+    POST_ARN_FIN = 3,    // after arn_finalize (column j+1)
+    POST_LAN = 4,        // after l2; fused flag in `flag`
+    POST_LAN_FIN = 5     // after lan_finalize (column j+1)
+};
+void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, hipStream_t s);
+void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
+                      int t, hipStream_t s);
+void launch_spmv(const int* rowptr, const int* col, const double* val, const double* x, double* y,
+                 int64_t n, hipStream_t s);
+
+// record field offsets (see include/tk.h)
+__host__ __device__ inline int rec_len(int kmax) { return 2 * kmax + 10; }
+__host__ __device__ inline int rec_gram(int kmax) { return kmax + 2; }
+__host__ __device__ inline int rec_bt(int kmax) { return 2 * kmax + 4; }
+__host__ __device__ inline int rec_col(int kmax) { return 2 * kmax + 5; }
+__host__ __device__ inline int rec_beta(int kmax) { return 2 * kmax + 6; }
+__host__ __device__ inline int rec_loss(int kmax) { return 2 * kmax + 7; }
+__host__ __device__ inline int rec_flag(int kmax) { return 2 * kmax + 8; }
+__host__ __device__ inline int rec_tracked(int kmax) { return 2 * kmax + 9; }
+
+}  // namespace tk
+
+#endif

@@ -1,0 +1,268 @@
+"""Compressed-side (k-sized) host numerics of tensorkrylov!.
+
+Restates, vectorized, the reference's per-iteration host work on the projected
+system (none of it touches n-length data):
+  * SpectralData / update_data!            src/eigenvalues.jl:247-370
+  * ApproximationData / compute_rank! /
+    exponential_sum_parameters!            src/approximation.jl:6-175
+  * solve_compressed_system                src/tensor_krylov_method.jl:10-34,
+                                           src/utils.jl:501-523
+  * residualnorm! / compressed_residual /
+    MVnorm / tensorinnerprod               src/utils.jl:132-443 (Lemma 3.4)
+Differences from the reference are performance-only: the coefficient tables are loaded
+once (the reference re-reads the CSV every iteration, src/approximation.jl:162-163);
+exp(gamma_j * Symmetric(H)) for all t terms comes from ONE eigendecomposition
+(exp(gH) = Q exp(g L) Q'); the O(d^3 t^2) masked products become leave-one-out /
+leave-two-out elementwise products.  Exact-arithmetic results are identical.
+"""
+import math
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class CompressedNormBreakdown(Exception):
+    """src/utils.jl:7-14: the compressed squared residual came out negative."""
+
+    def __init__(self, r_comp):
+        super().__init__("compressed norm breakdown: r_comp = %r" % r_comp)
+        self.r_comp = r_comp
+
+
+# ------------------------------------------------------------------ spectral data
+
+def laplace_eigenvalue(n, k, j):
+    """src/eigenvalues.jl:247-256: eigenvalue j of the k x k minor of the n-point Laplacian."""
+    h = 1.0 / (n + 1)
+    return 4 * (1.0 / (h * h)) * math.sin(j * math.pi * (1.0 / (2 * (k + 1)))) ** 2
+
+
+class SpectralData:
+    """SpectralData{matT,T,U} (src/eigenvalues.jl:268-284) with update_data!
+    (:353-370).  lambda_min/max/kappa of d * A_s[1:k,1:k]."""
+
+    def __init__(self, A, nmax):
+        self.A = A
+        self.symmetric = A.symmetric
+        self.lmin = np.full(nmax, np.inf)
+        self.lmax = np.full(nmax, np.inf)
+        self.kappa = np.full(nmax, np.inf)
+        self.k = 1
+        self._dense = None
+
+    def _minor(self, k):
+        from .structures import csc_leading_block
+        return csc_leading_block(self.A[0], k)
+
+    def update(self, d):
+        self.k += 1
+        k = self.k
+        cls = self.A.matrixclass
+        n = self.A.dimensions()[0]
+        if self.symmetric:
+            if cls in ("Laplace", "LaplaceDense"):
+                lo = laplace_eigenvalue(n, k, 1) * d              # analytic_eigenvalues :258-265
+                hi = laplace_eigenvalue(n, k, k) * d
+            else:
+                ev = np.linalg.eigvalsh(self._minor(k))           # :337
+                lo, hi = ev.min() * d, ev.max() * d
+            self.lmin[k - 1], self.lmax[k - 1] = lo, hi
+            self.kappa[k - 1] = hi * (1.0 / lo)                   # :360
+        else:
+            ev = np.linalg.eigvals(self._minor(k))                # :344-350
+            if np.all(ev.imag == 0):
+                ev = ev.real
+            self.lmin[k - 1] = float(np.min(ev)) * d
+
+    def current(self):
+        k = self.k
+        return self.lmin[k - 1], self.lmax[k - 1], self.kappa[k - 1]
+
+
+# ------------------------------------------------------------------ exp-sum approximation
+
+class ExpSumTables:
+    """coefficients_data (packed by data/pack_tables.py), loaded once."""
+
+    _cache = None
+
+    def __init__(self, path=None):
+        path = path or os.path.join(_HERE, "data", "expsum_tables.npz")
+        z = np.load(path, allow_pickle=False)
+        self.R = np.asarray(z["R"])
+        self.err = np.asarray(z["err"])
+        self._z = z
+        self._coef = {}
+
+    @classmethod
+    def default(cls):
+        if cls._cache is None:
+            cls._cache = cls()
+        return cls._cache
+
+    def coefficients(self, rank, digit, order):
+        key = "xk%02d.%d_%d" % (rank, digit, order)         # 1_xk{t:02d}.{digit}_{order}
+        if key not in self._coef:
+            v = np.asarray(self._z[key])
+            self._coef[key] = (v[rank:2 * rank].copy(), v[:rank].copy())   # alpha, omega
+        return self._coef[key]
+
+
+def parse_condition(kappa):
+    """src/approximation.jl:109-116."""
+    order = int(math.floor(math.log10(kappa)))
+    digit = int(math.floor(kappa / (10.0 ** order)))
+    return order, digit
+
+
+class ApproximationData:
+    """ApproximationData{T,U} (src/approximation.jl:6-30): rank t and (alpha, omega)
+    with 1/x ~ sum_j omega_j exp(-alpha_j x)."""
+
+    def __init__(self, tol, symmetric, tables=None):
+        self.tol = tol
+        self.symmetric = symmetric
+        self.tables = tables if tables is not None or not symmetric else ExpSumTables.default()
+        self.rank = 0
+        self.alpha = np.zeros(1)
+        self.omega = np.zeros(1)
+        self.first_digit = 0
+        self.condition_order = 0
+
+    def update(self, spectral):
+        lmin, _, kappa = spectral.current()
+        if self.symmetric:
+            # compute_rank! (:65-84) + exponential_sum_parameters! (:119-147)
+            order, digit = parse_condition(kappa)
+            R = self.tables.R
+            while True:
+                rows = np.nonzero(R == digit * 10.0 ** order)[0]
+                if len(rows):
+                    break
+                digit += 1
+                if digit > 100:
+                    raise ValueError("condition number %r beyond the coefficient tables" % kappa)
+            errs = self.tables.err[rows[0]]
+            ok = np.nonzero(self.tol >= errs)[0]
+            if len(ok) == 0:
+                raise ValueError("no tabulated rank reaches tol=%g at kappa=%g" % (self.tol, kappa))
+            self.rank = int(ok.min()) + 1
+            self.first_digit, self.condition_order = digit, order
+            self.alpha, self.omega = self.tables.coefficients(self.rank, digit, order)
+        else:
+            # compute_rank!(::NonSym) (:86-107) + closed form (:150-158)
+            rank = 1
+            while 2.75 * (1.0 / lmin) * math.exp(-math.pi * math.sqrt(rank / 2)) > self.tol:
+                rank += 1
+            self.rank = rank
+            h = math.pi * (1.0 / math.sqrt(rank))
+            js = np.arange(-rank, rank + 1, dtype=np.float64)
+            self.alpha = np.log(np.exp(js * h) + np.sqrt(1 + np.exp(2 * js * h)))
+            self.omega = h * (1.0 / np.sqrt(1 + np.exp(-2 * js * h)))
+
+
+# ------------------------------------------------------------------ compressed solve
+
+def solve_compressed_system(H1, btilde, approx, lmin, symmetric):
+    """y = sum_j omega_j/lmin * exp(-alpha_j/lmin * first(H)) btilde_s, as the Kruskal
+    tensor (lambda, [Y_s]) of src/tensor_krylov_method.jl:10-34.  first(H) is
+    Symmetric(H_1, :L) for SymInstance (src/tensor_struct.jl:259)."""
+    lam_inv = 1.0 / lmin
+    lam = lam_inv * approx.omega
+    gam = -approx.alpha * lam_inv
+    B = np.stack(btilde, axis=1)                       # k x d
+    if symmetric:
+        L = np.tril(H1)
+        S = L + np.tril(L, -1).T
+        w, Q = np.linalg.eigh(S)
+        C = Q.T @ B                                    # k x d
+        E = np.exp(np.outer(w, gam))                   # k x t
+        Ys = [Q @ (E * C[:, s:s + 1]) for s in range(B.shape[1])]
+    else:
+        import scipy.linalg
+        t = len(gam)
+        Ys = [np.empty((H1.shape[0], t)) for _ in range(B.shape[1])]
+        for j in range(t):
+            Ej = scipy.linalg.expm(gam[j] * H1)
+            P = Ej @ B
+            for s in range(B.shape[1]):
+                Ys[s][:, j] = P[:, s]
+    return lam, Ys
+
+
+# ------------------------------------------------------------------ residual (Lemma 3.4)
+
+def _leave_out(stack):
+    """pre[s] = prod_{q<s}, suf[s] = prod_{q>s} of a (d, t, t) stack (elementwise)."""
+    d = stack.shape[0]
+    one = np.ones_like(stack[0])
+    pre = [one]
+    for s in range(d - 1):
+        pre.append(pre[-1] * stack[s])
+    suf = [one] * d
+    acc = one
+    for s in range(d - 1, -1, -1):
+        suf[s] = acc
+        acc = acc * stack[s]
+    return pre, suf
+
+
+def residualnorm(Hs, lam, Ys, k, subdiag, btilde, b_norm):
+    """residualnorm! + compressed_residual (src/utils.jl:371-443).
+    Hs: d k x k minors (full), Ys: d k x t, subdiag[s] = H_s[k+1, k].
+    Returns (r_comp, r_norm); raises CompressedNormBreakdown when r_comp < 0."""
+    d = len(Ys)
+    t = len(lam)
+    Y = np.stack(Ys)                                   # d x k x t
+    Ly = np.tril(np.einsum("ski,skj->sij", Y, Y))      # lower(Y_s' Y_s)
+    Lam = np.tril(np.outer(lam, lam))
+    W = np.tril(np.full((t, t), 2.0), -1) + np.eye(t)  # weights: 1 on diag, 2 below
+    pre, suf = _leave_out(Ly)
+    loo = [pre[s] * suf[s] for s in range(d)]          # prod_{q != s} Ly_q
+    # first term: sum_s beta_s^2 * squared_tensor_entries(Ly[-s], Gamma_s)
+    res = 0.0
+    for s in range(d):
+        yk = Y[s, k - 1, :]
+        Gam = np.tril(np.outer(yk, yk)) * Lam
+        res += subdiag[s] ** 2 * float(np.sum(W * Gam * loo[s]))
+    # compressed residual
+    Z = np.einsum("sab,sbt->sat", np.stack(Hs), Y)     # Z_s = H_s Y_s
+    X = np.einsum("ski,skj->sij", Y, Z)                # X_s = Y_s' Z_s
+    Lz = np.tril(np.einsum("ski,skj->sij", Z, Z))
+    term = np.zeros((t, t))
+    for s in range(d):
+        term += loo[s] * Lz[s]
+    for s in range(d):
+        for r in range(d):
+            if r == s:
+                continue
+            a, b = (s, r) if s < r else (r, s)
+            mid = np.ones((t, t))
+            for q in range(a + 1, b):
+                mid = mid * Ly[q]
+            term += pre[a] * mid * suf[b] * X[s] * X[r].T
+    hy_norm = float(np.sum(W * Lam * term))
+    F0 = Y[:, 0, :]                                    # first rows  d x t
+    G0 = Z[:, 0, :]
+    fpre = np.ones_like(F0)
+    for s in range(1, d):
+        fpre[s] = fpre[s - 1] * F0[s - 1]
+    fsuf = np.ones_like(F0)
+    for s in range(d - 2, -1, -1):
+        fsuf[s] = fsuf[s + 1] * F0[s + 1]
+    hy_b = float(np.sum(lam[None, :] * G0 * fpre * fsuf)) * b_norm
+    bnorm2 = float(np.prod([np.dot(b, b) for b in btilde]))
+    r_comp = hy_norm - 2 * hy_b + bnorm2
+    if r_comp < 0.0:
+        raise CompressedNormBreakdown(r_comp)
+    return r_comp, math.sqrt(res + r_comp)
+
+
+def orthogonality_loss_from_gram(G, k):
+    """norm(V[:,1:k]'V[:,1:k] - I) (src/orthogonal_bases.jl:250-257) from the lower
+    Gram rows G[c, 0..c] kept by the device."""
+    Gk = np.tril(G[:k, :k])
+    D = Gk + np.tril(Gk, -1).T - np.eye(k)
+    return float(np.linalg.norm(D))

@@ -1,0 +1,184 @@
+"""TensorArnoldi / TensorLanczos / TensorLanczosReorth backed by libtkhip.
+
+Mirrors src/decompositions.jl:120-176 and the fan-out orthonormalize!(td, b) /
+orthonormalize!(td, k) of src/orthogonal_bases.jl:142-180.  The n-length state
+(V_s, b_s, work vectors) lives on the device; the host keeps only what the
+reference's driver reads on the host: H_s (k x k minors and H_s[k+1,k]), btilde_s,
+and factor 1's Gram rows for orthogonality_data.  H is updated from the per-step
+records with the reference's bookkeeping (update_subdiagonals!, the LanczosReorth
+zeroing of H[1:k-2, k]).
+"""
+import numpy as np
+
+from . import _lib as L
+from .device import Context, DeviceDecomposition, DeviceMatrix
+
+
+class Partition:
+    """Contiguous factor blocks over ranks: the first d % N ranks own
+    ceil(d/N) factors, the rest floor(d/N)."""
+
+    def __init__(self, d, nranks=1, rank=0):
+        self.d, self.nranks, self.rank = d, nranks, rank
+        q, r = divmod(d, nranks)
+        self.sizes = [q + (1 if i < r else 0) for i in range(nranks)]
+        self.starts = [sum(self.sizes[:i]) for i in range(nranks)]
+
+    @property
+    def first(self):
+        return self.starts[self.rank]
+
+    @property
+    def nf(self):
+        return self.sizes[self.rank]
+
+    def local(self):
+        return range(self.first, self.first + self.nf)
+
+
+class TensorDecomposition:
+    method = None
+    name = None
+
+    def __init__(self, A, nmax, ctx=None, partition=None, track_all_gram=False, backend=None):
+        self.A = A
+        self.d = len(A)
+        self.n = A.dimensions()[0]
+        self.kmax = nmax
+        self.part = partition or Partition(self.d)
+        self.layout = L.RecordLayout(nmax)
+        KP, KC = nmax + 2, nmax + 1
+        self.H = np.zeros((self.d, KP, KC))
+        self.btilde = np.zeros((self.d, KC))
+        self.gram = {}
+        self.loss = np.zeros((self.d, KC))
+        self.reorth = np.zeros((self.d, KC), dtype=bool)
+        self.track_all_gram = track_all_gram
+        self.ctx = ctx
+        self._backend = backend
+        self.dev = None
+
+    # -------------------------------------------------------------- device setup
+    def _attach(self, b):
+        if self._backend is not None:           # injected (tests of the host logic only)
+            self.dev = self._backend(self, b)
+            return
+        if self.ctx is None:
+            self.ctx = Context(0)
+        mats = {}
+        dmats = []
+        for s in self.part.local():
+            key = id(self.A[s])
+            if key not in mats:                 # factors sharing A_s share its device CSR
+                mats[key] = DeviceMatrix(self.ctx, self.A[s])
+            dmats.append(mats[key])
+        self._dmats = list(mats.values())
+        self.dev = DeviceDecomposition(self.ctx, self.method, self.d, self.part.first, dmats,
+                                       [b[s] for s in self.part.local()], self.kmax,
+                                       track_all_gram=self.track_all_gram)
+
+    # -------------------------------------------------------------- records -> host mirror
+    def _apply_gram(self, rec):
+        lay = self.layout
+        for s in range(self.d):
+            c = int(round(rec[s, lay.col]))
+            if c < 0:
+                continue
+            self.btilde[s, c] = rec[s, lay.bt]
+            if rec[s, lay.tracked] > 0:
+                G = self.gram.setdefault(s, np.zeros((self.kmax + 1, self.kmax + 1)))
+                G[c, :c + 1] = rec[s, lay.gram:lay.gram + c + 1]
+
+    def _apply_step(self, j, rec):
+        raise NotImplementedError
+
+    # -------------------------------------------------------------- reference API
+    def orthonormalize_first(self, b):
+        """orthonormalize!(td, b) (src/orthogonal_bases.jl:142-160): V[:,1] = b/|b|,
+        then step 1 for every factor."""
+        self._attach(b)
+        self._apply_gram(self.dev.init())
+        self.orthonormalize(1)
+
+    def orthonormalize(self, k):
+        """orthonormalize!(td, k) (src/orthogonal_bases.jl:162-180), k 1-based."""
+        j = k - 1
+        rec = self.dev.step(j)
+        self._apply_step(j, rec)
+        self._apply_gram(rec)
+
+    def flush(self):
+        rec = self.dev.flush()
+        self._apply_gram(rec)
+
+    def subdiagonal(self, k):
+        return [self.H[s, k, k - 1] for s in range(self.d)]
+
+    def minors(self, k):
+        """compute_minors (src/utils.jl:490-498): H_s[1:k,1:k] for every factor."""
+        return [self.H[s, :k, :k].copy() for s in range(self.d)]
+
+    def orthogonality_loss(self, s, k):
+        from .compressed import orthogonality_loss_from_gram
+        return orthogonality_loss_from_gram(self.gram[s], k)
+
+    def basis(self, s, k):
+        """V_s[:, 1:k] (local factor s only)."""
+        f = s - self.part.first
+        assert 0 <= f < self.part.nf, "factor %d is not owned by this rank" % s
+        return self.dev.basis(f, 0, k)
+
+    def close(self):
+        if self.dev is not None and hasattr(self.dev, "close"):
+            self.dev.close()
+        for m in getattr(self, "_dmats", []):
+            m.close()
+
+
+class TensorArnoldi(TensorDecomposition):
+    """src/decompositions.jl:120-137 -- MGS steps (src/orthogonal_bases.jl:15-37)."""
+    method = L.TK_ARNOLDI
+    name = "TensorArnoldi"
+
+    def _apply_step(self, j, rec):
+        for s in range(self.d):
+            self.H[s, :j + 2, j] = rec[s, :j + 2]
+
+
+class TensorLanczos(TensorDecomposition):
+    """src/decompositions.jl:140-157 -- TTR steps (src/orthogonal_bases.jl:39-67)."""
+    method = L.TK_LANCZOS
+    name = "TensorLanczos"
+
+    def _apply_step(self, j, rec):
+        for s in range(self.d):
+            alpha, beta = rec[s, j], rec[s, j + 1]
+            self.H[s, j, j] = alpha                      # :50
+            self.H[s, j + 1, j] = beta                   # update_subdiagonals! (decompositions.jl:180-186)
+            self.H[s, j, j + 1] = beta
+
+
+class TensorLanczosReorth(TensorDecomposition):
+    """src/decompositions.jl:159-176 -- TTR + loss check + MGS redo
+    (src/orthogonal_bases.jl:98-139)."""
+    method = L.TK_LANCZOS_REORTH
+    name = "TensorLanczosReorth"
+
+    def _apply_step(self, j, rec):
+        lay = self.layout
+        for s in range(self.d):
+            self.loss[s, j] = rec[s, lay.loss]
+            if rec[s, lay.flag] > 0:
+                self.reorth[s, j] = True
+                self.H[s, :j + 2, j] = rec[s, :j + 2]    # MGS column (:125)
+                beta = self.H[s, j + 1, j]               # :127
+                self.H[s, :max(j - 1, 0), j] = 0.0       # H[1:k-2, k] .= 0 (:129)
+            else:
+                self.H[s, j, j] = rec[s, j]
+                beta = rec[s, j + 1]
+            self.H[s, j + 1, j] = beta                   # update_subdiagonals! (:137)
+            self.H[s, j, j + 1] = beta
+
+
+METHODS = {"TensorArnoldi": TensorArnoldi, "TensorLanczos": TensorLanczos,
+           "TensorLanczosReorth": TensorLanczosReorth}

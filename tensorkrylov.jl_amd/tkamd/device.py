@@ -1,0 +1,173 @@
+"""Device objects owning libtkhip handles: context, coefficient matrix, decomposition.
+
+These wrap include/tk.h one to one; the Julia glue (julia/TensorKrylovHIP.jl) binds
+the same entry points with ccall.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+
+class Context:
+    """tk_ctx: one HIP device + one stream (+ optional RCCL communicator)."""
+
+    def __init__(self, device=0):
+        self._lib = L.lib()
+        h = ctypes.c_void_p()
+        L.check(self._lib.tk_ctx_create(int(device), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self.nranks = 1
+        self.rank = 0
+
+    def sync(self):
+        L.check(self._lib.tk_ctx_sync(self.h))
+
+    def init_comm(self, uid, nranks, rank):
+        assert len(uid) == 128
+        L.check(self._lib.tk_comm_init(self.h, uid, int(nranks), int(rank)))
+        self.nranks, self.rank = nranks, rank
+
+    def allreduce_host(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        L.check(self._lib.tk_comm_allreduce_host(self.h, L.dptr(arr), arr.size))
+        return arr
+
+    def timing(self, level):
+        L.check(self._lib.tk_timing_enable(self.h, int(level)))
+
+    def timing_read(self, cls):
+        ms = ctypes.c_double()
+        cnt = ctypes.c_long()
+        L.check(self._lib.tk_timing_read(self.h, int(cls), ctypes.byref(ms), ctypes.byref(cnt)))
+        return ms.value, cnt.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.tk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def unique_id():
+    buf = ctypes.create_string_buffer(128)
+    L.check(L.lib().tk_comm_unique_id(buf))
+    return buf.raw
+
+
+class DeviceMatrix:
+    """tk_mat: A_s on the device as CSR (from Julia-style CSC)."""
+
+    def __init__(self, ctx, csc, one_based=False):
+        colptr, rowval, nzval = (np.ascontiguousarray(csc[0], dtype=np.int64),
+                                 np.ascontiguousarray(csc[1], dtype=np.int64),
+                                 np.ascontiguousarray(csc[2], dtype=np.float64))
+        self.ctx = ctx
+        self.n = len(colptr) - 1
+        h = ctypes.c_void_p()
+        L.check(ctx._lib.tk_matrix_from_csc(ctx.h, self.n, L.i64ptr(colptr), L.i64ptr(rowval),
+                                            L.dptr(nzval), 1 if one_based else 0, ctypes.byref(h)))
+        self.h = h
+
+    def matvec(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty(self.n)
+        L.check(self.ctx._lib.tk_matvec(self.h, L.dptr(x), L.dptr(y)))
+        return y
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx._lib.tk_matrix_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceDecomposition:
+    """tk_decomp: this rank's factors s = first .. first+nf-1 of a d_total-factor
+    tensor decomposition, with device-resident V_s (n x kmax+1), b_s and work vectors."""
+
+    def __init__(self, ctx, method, d_total, first, mats, bs, kmax, track_all_gram=False):
+        self.ctx = ctx
+        self.method = method
+        self.d_total = d_total
+        self.first = first
+        self.nf = len(mats)
+        self.n = mats[0].n
+        self.kmax = kmax
+        self.layout = L.RecordLayout(kmax)
+        self.m = self.layout.m
+        self._bs = [np.ascontiguousarray(b, dtype=np.float64) for b in bs]
+        MatArr = ctypes.c_void_p * self.nf
+        BArr = ctypes.POINTER(ctypes.c_double) * self.nf
+        marr = MatArr(*[m.h.value for m in mats])
+        barr = BArr(*[L.dptr(b) for b in self._bs])
+        h = ctypes.c_void_p()
+        L.check(ctx._lib.tk_decomp_create(ctx.h, int(method), int(d_total), int(first), self.nf, marr,
+                                          barr, int(self.n), int(kmax), 1 if track_all_gram else 0,
+                                          ctypes.byref(h)))
+        self.h = h
+        self._mats = mats
+
+    def _rec(self):
+        return np.zeros((self.d_total, self.m))
+
+    def init(self, want=True):
+        r = self._rec() if want else None
+        L.check(self.ctx._lib.tk_decomp_init(self.h, L.dptr(r)))
+        return r
+
+    def step(self, j, want=True):
+        r = self._rec() if want else None
+        L.check(self.ctx._lib.tk_decomp_step(self.h, int(j), L.dptr(r)))
+        return r
+
+    def sweep(self, j0, j1):
+        L.check(self.ctx._lib.tk_decomp_sweep(self.h, int(j0), int(j1)))
+
+    def flush(self, want=True):
+        r = self._rec() if want else None
+        L.check(self.ctx._lib.tk_decomp_flush(self.h, L.dptr(r)))
+        return r
+
+    def records(self, s0, s1):
+        out = np.zeros((s1 - s0, self.d_total, self.m))
+        L.check(self.ctx._lib.tk_decomp_records(self.h, int(s0), int(s1), L.dptr(out)))
+        return out
+
+    def basis(self, f, c0, nc):
+        out = np.zeros((nc, self.n))          # column-major n x nc == row-major nc x n
+        L.check(self.ctx._lib.tk_decomp_get_basis(self.h, int(f), int(c0), int(nc), L.dptr(out)))
+        return out.T
+
+    def basis_mul(self, k, Ys, want=True):
+        """X_s = V_s[:, :k] @ Y_s for the local factors (Ys: list of k x t arrays)."""
+        t = Ys[0].shape[1]
+        Y = np.ascontiguousarray(np.stack([np.asarray(y, dtype=np.float64).T for y in Ys]))  # [nf][t][k]
+        X = np.zeros((self.nf, t, self.n)) if want else None
+        L.check(self.ctx._lib.tk_decomp_basis_mul(self.h, int(k), int(t), L.dptr(Y), L.dptr(X)))
+        if not want:
+            return None
+        return [X[f].T.copy() for f in range(self.nf)]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx._lib.tk_decomp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
