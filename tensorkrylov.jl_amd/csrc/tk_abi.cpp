@@ -318,10 +318,13 @@ struct tk_decomp {
     std::vector<tk_mat*> mats;
     std::vector<DFac> hf;   // host copy of descriptors
     DFac* df = nullptr;     // device descriptors
+    DFac* dsub = nullptr;   // scratch descriptor array (LanczosReorth redo subset)
     std::vector<void*> allocs;
-    double* rec = nullptr;  // [(kmax+2) slots][d_total][m]
+    double* rec = nullptr;   // send records [(kmax+2) slots][d_total][m] (local rows only)
+    double* recv = nullptr;  // all-reduced records (== rec on a single rank)
     double* Ydev = nullptr; size_t ycap = 0;
     double* Xdev = nullptr; size_t xcap = 0;
+    double* scratch = nullptr;   // column gather buffer (n x 8)
     // host Gram mirror (LanczosReorth decisions): [nf][(kmax+1)^2]
     std::vector<std::vector<double>> gram;
 };
@@ -339,6 +342,9 @@ static tk_status dalloc(tk_decomp* dc, void** p, size_t bytes) {
 
 static void free_decomp(tk_decomp* dc) {
     for (void* p : dc->allocs) hipFree(p);
+    if (dc->scratch) hipFree(dc->scratch);
+    if (dc->Ydev) hipFree(dc->Ydev);
+    if (dc->Xdev) hipFree(dc->Xdev);
     delete dc;
 }
 
@@ -385,7 +391,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.rowptr = mats[f]->rowptr;
         d.col = mats[f]->col;
         d.val = mats[f]->val;
-        DA(d.V, (size_t)dc->ld * KC * sizeof(double));
+        DA(d.V, (size_t)dc->ntiles * 256 * KC * sizeof(double));   // tile-major
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
         hipError_t e = hipMemcpy(bb, b[f], n * sizeof(double), hipMemcpyHostToDevice);
@@ -406,11 +412,16 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.gidx = gi;
     }
     DA(dc->df, nf * sizeof(DFac));
+    DA(dc->dsub, nf * sizeof(DFac));
     {
         hipError_t e = hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice);
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
     }
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+    if (c->comm && c->nranks > 1)
+        DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+    else
+        dc->recv = dc->rec;
 #undef DA
     if (method == TK_LANCZOS_REORTH) dc->gram.assign(nf, std::vector<double>((size_t)KC * KC, 0.0));
     *out = dc;
@@ -438,16 +449,20 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     return a;
 }
 
+// One RCCL all-reduce per record slot: the send buffer holds only this rank's rows
+// (other rows stay zero forever), so the sum is exact and every rank receives every
+// factor's record.
 static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out) {
     tk_ctx* c = dc->ctx;
-    double* s = dc->rec + (size_t)slot * dc->d_total * dc->m;
     const size_t cnt = (size_t)dc->d_total * dc->m;
-    if (c->comm && c->nranks > 1) {
+    double* s = dc->rec + (size_t)slot * cnt;
+    double* r = dc->recv + (size_t)slot * cnt;
+    if (dc->recv != dc->rec) {
         Timer tm(c, TCLS_XCH, 2);
-        NCCLCHK(ncclAllReduce(s, s, cnt, ncclDouble, ncclSum, c->comm, c->stream));
+        NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->stream));
     }
     if (rec_out) {
-        HIPCHK(hipMemcpyAsync(rec_out, s, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
     return TK_OK;
@@ -471,16 +486,15 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    tk_status st = clear_slot(dc, 0);
-    if (st) return st;
+    tk_status st = TK_OK;
     KArgs a = base_args(dc, 0, 0);
     const int nf = dc->nf;
     RUN(TCLS_PASS1, 2, launch_init_a(dc->df, nf, a, s), "init_a");
     RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
-    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_A, 0, s), "post");
+    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_A, 0, 0, s), "post");
     RUN(TCLS_PASS1, 2, launch_init_b(dc->df, nf, a, s), "init_b");
     RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2, dc->npart, s), "reduce");
-    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, s), "post");
+    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, 1, s), "post");
     dc->inited = true;
     dc->jnext = 0;
     dc->pending = false;
@@ -506,11 +520,11 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
     if (dc->method == TK_ARNOLDI) {
         RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, a, s), "arn_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, 1, s), "post");
     } else {
         RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, 1, s), "post");
     }
     return TK_OK;
 }
@@ -530,8 +544,6 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_ctx* c = dc->ctx;
     hipStream_t s = c->stream;
     const int nf = dc->nf, slot = j + 1;
-    tk_status st = clear_slot(dc, slot);
-    if (st) return st;
     KArgs a = base_args(dc, j, slot);
     Timer step_timer(c, TCLS_STEP, 1);
     if (dc->method == TK_ARNOLDI) {
@@ -545,7 +557,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         }
         RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, j + 2, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;
@@ -558,7 +570,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         }
         RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, fused ? 1 : 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else {
         // TensorLanczosReorth (src/orthogonal_bases.jl:98-139): TTR, write v_{j+1},
@@ -567,10 +579,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
         RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, 0, 1, s), "post");
         RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, 0, s), "post");
         const size_t cnt = (size_t)dc->d_total * dc->m;
         std::vector<double> r(cnt);
         double* slotp = a.rec;
@@ -594,19 +606,17 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             std::vector<DFac> sub;
             for (int f = 0; f < nf; ++f)
                 if (redo[f]) sub.push_back(dc->hf[f]);
-            DFac* dsub = nullptr;
-            HIPCHK(hipMallocAsync((void**)&dsub, sub.size() * sizeof(DFac), s));
-            HIPCHK(hipMemcpyAsync(dsub, sub.data(), sub.size() * sizeof(DFac), hipMemcpyHostToDevice, s));
+            DFac* dsub = dc->dsub;
+            HIPCHK(hipMemcpy(dsub, sub.data(), sub.size() * sizeof(DFac), hipMemcpyHostToDevice));
             const int ns = (int)sub.size();
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dsub, ns, a, s), "arn_a1_plain");
             RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 1, dc->npart, s), "reduce");
             RUN(TCLS_PASS2, 2, launch_arn_a2(dsub, ns, a, s), "arn_a2");
             RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 2, j + 2, dc->npart, s), "reduce");
-            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN, 0, s), "post");
+            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN, 0, 1, s), "post");
             RUN(TCLS_FIN, 2, launch_arn_finalize(dsub, ns, a, s), "arn_finalize");
             RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 3, dc->npart, s), "reduce");
-            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN_FIN, 0, s), "post");
-            HIPCHK(hipFreeAsync(dsub, s));
+            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN_FIN, 0, 0, s), "post");
             HIPCHK(hipMemcpyAsync(r.data(), slotp, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));
             for (int f = 0; f < nf; ++f) {
@@ -664,10 +674,8 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {
         }
         return TK_OK;
     }
-    tk_status st = clear_slot(dc, slot);
-    if (st) return st;
     KArgs a = base_args(dc, dc->last_j, slot);
-    st = finalize_pending(dc, a);
+    tk_status st = finalize_pending(dc, a);
     if (st) return st;
     dc->pending = false;
     return exchange_and_copy(dc, slot, rec_out);
@@ -678,7 +686,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
     CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
     HIPCHK(hipSetDevice(dc->ctx->device));
     const size_t per = (size_t)dc->d_total * dc->m;
-    HIPCHK(hipMemcpyAsync(out, dc->rec + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                           dc->ctx->stream));
     HIPCHK(hipStreamSynchronize(dc->ctx->stream));
     return TK_OK;
@@ -693,10 +701,22 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;
     }
+    if (nc == 0) return TK_OK;
     const DFac& d = dc->hf[f];
-    HIPCHK(hipMemcpy2DAsync(out, dc->n * sizeof(double), d.V + (size_t)c0 * dc->ld, dc->ld * sizeof(double),
-                            dc->n * sizeof(double), nc, hipMemcpyDeviceToHost, dc->ctx->stream));
-    HIPCHK(hipStreamSynchronize(dc->ctx->stream));
+    hipStream_t s = dc->ctx->stream;
+    // gather GCH columns at a time from the tile-major basis into a persistent scratch
+    const int GCH = 8;
+    if (!dc->scratch) {
+        HIPCHK(hipMalloc((void**)&dc->scratch, (size_t)dc->n * GCH * sizeof(double)));
+    }
+    for (int cc = 0; cc < nc; cc += GCH) {
+        const int m = std::min(GCH, nc - cc);
+        launch_get_cols(d.V, dc->n, dc->kmax, c0 + cc, m, dc->scratch, s);
+        LAUNCHCHK("get_cols");
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(out + (size_t)cc * dc->n, dc->scratch, (size_t)dc->n * m * sizeof(double),
+                         hipMemcpyDeviceToHost));
+    }
     return TK_OK;
 }
 
@@ -727,11 +747,11 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
     KArgs a = base_args(dc, 0, 0);
     RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");
     if (X) {
-        for (int f = 0; f < dc->nf; ++f)
-            HIPCHK(hipMemcpy2DAsync(X + (size_t)f * dc->n * t, dc->n * sizeof(double),
-                                    dc->Xdev + (size_t)f * dc->ld * t, dc->ld * sizeof(double),
-                                    dc->n * sizeof(double), t, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        for (int f = 0; f < dc->nf; ++f)
+            HIPCHK(hipMemcpy2D(X + (size_t)f * dc->n * t, dc->n * sizeof(double),
+                               dc->Xdev + (size_t)f * dc->ld * t, dc->ld * sizeof(double),
+                               dc->n * sizeof(double), t, hipMemcpyDeviceToHost));
     }
     return TK_OK;
 }

@@ -23,7 +23,7 @@ struct DFac {
     const int* rowptr;    // CSR of A_s (n+1)
     const int* col;       // (nnz) ascending within a row
     const double* val;    // (nnz)
-    double* V;            // basis, column-major, ld x (kmax+1)
+    double* V;            // basis, tile-major: (r/256)*256*(kmax+1) + c*256 + r%256
     const double* b;      // b_s (n)
     double* W;            // work vector (SpMV output / Lanczos v)
     double* U;            // work vector (w' / Lanczos u)
@@ -41,7 +41,7 @@ struct DFac {
 
 struct KArgs {
     int64_t n;        // rows
-    int64_t ld;       // leading dimension of V (n rounded up to 256)
+    int64_t ld;       // padded length of every n-vector (n rounded up to 256)
     int j;            // step (0-based column)
     int npart;        // partial blocks per factor (function of n only)
     int ntiles;       // ceil(n / 256)
@@ -71,7 +71,8 @@ enum PostKind {
     POST_LAN = 4,        // after l2; fused flag in `flag`
     POST_LAN_FIN = 5     // after lan_finalize (column j+1)
 };
-void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, hipStream_t s);
+void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s);
+void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s);
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s);
 void launch_spmv(const int* rowptr, const int* col, const double* val, const double* x, double* y,

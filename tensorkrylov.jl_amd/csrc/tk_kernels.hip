@@ -1,22 +1,28 @@
 // tk_kernels.hip -- gfx950 (MI355X) kernels for the inner Krylov iteration of
-// thbake/TensorKrylov.jl.  Written for CDNA4: 64-lane waves, 256-thread blocks,
-// thread-per-row streaming of the column-major basis V (n x (kmax+1), ld = n rounded
-// up to 256) with the row held in VGPRs, deterministic LDS-transpose block reductions,
-// and f64 MFMA (v_mfma_f64_16x16x4_f64) for the tall-skinny V*Y product.
+// thbake/TensorKrylov.jl.
+//
+// Layout (DESIGN.md "Data layout in HBM"): the basis V_s of every factor is stored
+// TILE-MAJOR: rows are cut into 256-row tiles and each tile holds its kmax+1 columns
+// contiguously, element (r, c) at  (r/256)*256*(kmax+1) + c*256 + r%256.  A 256-thread
+// block owns one tile at a time; thread t keeps its row V[r, 0..ncols) in VGPRs,
+// loaded with buffer_load_dwordx2 whose hardware range check (num_records =
+// ncols*2 KiB from the tile base) zero-fills the columns a step does not use -- no
+// per-column predicates, one 32-bit VGPR offset per load, and a whole tile's columns
+// inside one 2 MiB page.  All n-length vectors are padded to whole tiles (zeros).
 //
 // Numerical scheme (DESIGN.md "Arnoldi step"): the reference's two-pass MGS
 // (src/orthogonal_bases.jl:15-37) is computed as CGS2 -- h1 = V'w, w' = w - V h1,
 // h2 = V'w', H[:,j] = h1 + h2, beta = sqrt(|w'|^2 - |h2|^2),
-// v_{j+1} = (w' - V h2) * inv(beta) -- equal to MGS2 in exact arithmetic and within
-// the parity tolerance in floating point (tests/test_gpu_parity.py).  The correction
-// v_{j+1} is not written by a pass of its own: the next step's SpMV kernel writes it
-// while it holds the same V rows in registers, applying A to w' and subtracting
-// A V h2 = V Hbar h2 through the Arnoldi relation.  V is therefore streamed twice per
-// step (the compulsory MGS2 traffic of SURVEY.md section 8d), not three times.
+// v_{j+1} = (w' - V h2) * inv(beta) -- equal to MGS2 in exact arithmetic and within the
+// parity tolerance in floating point (tests/test_gpu_parity.py).  v_{j+1} is not
+// written by a pass of its own: the next step's SpMV kernel writes it while it holds
+// the same V rows in registers, applying A to w' and subtracting A V h2 = V Hbar h2
+// through the Arnoldi relation.  V is streamed twice per step (the compulsory MGS2
+// traffic of SURVEY.md section 8d).
 //
-// Every reduction is fixed-order (per-block LDS transpose, then one wave per value
-// over NPART block partials, NPART a function of n only), so results are bitwise
-// reproducible run to run and independent of how the factors are split over GPUs.
+// Every reduction is fixed-order (LDS transpose + DPP row sums per block, then one
+// wave per value over NPART block partials, NPART a function of n only): results are
+// bitwise reproducible and independent of how the factors are split over GPUs.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -26,16 +32,25 @@
 namespace tk {
 
 #define TPB 256          // threads per block == rows per tile
-#define CH 16            // columns per block-reduction chunk
-#define TSTR (TPB + 16)  // LDS row stride (doubles): the +32 dwords put the two 32-lane
-                         // halves of a ds_read_b64 on disjoint banks
+#define CH 16            // values per block-reduction chunk
+#define TSTR (TPB + 16)  // LDS stride (doubles) of the transpose buffer
+#define COEF_PAD(kmax) ((kmax) + 2 > 64 ? (kmax) + 2 : 64)   // LDS coefficient array length
 
-// ------------------------------------------------------------------ small helpers
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+#define GP(T, p) ((__attribute__((address_space(1))) T*)(p))
 
-// Julia's CSC scatter adds nz*x into y without FMA; keep the product and the sum
-// separately rounded so the device SpMV matches it bit for bit.  (__dmul_rn/__dadd_rn
-// are plain * and + in ROCm 7.2's headers, so contraction must be switched off with
-// the pragma at every use site.)
+// ------------------------------------------------------------------ primitives
+
+__device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bld(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
+// Julia's CSC scatter adds nz*x into y without FMA; keep products and sums separately
+// rounded so the device SpMV equals it bit for bit (__dmul_rn/__dadd_rn are plain
+// * and + in ROCm 7.2's headers, so contraction is switched off explicitly).
 __device__ __forceinline__ double mul_rn(double a, double b) {
 #pragma clang fp contract(off)
     return a * b;
@@ -45,9 +60,25 @@ __device__ __forceinline__ double add_rn(double a, double b) {
     return a + b;
 }
 
-// Accumulate, over the block's 256 rows, CH per-thread values x[0..CH) into acc[base..]
-// (LDS).  Fixed order: lane (col*16+part) sums elements q*16+part, q ascending, of
-// column col, then a 16-lane xor butterfly.
+// DPP row rotate (16-lane rows) of a double.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+// Sum over each 16-lane row; every lane of the row ends with its row's total.
+__device__ __forceinline__ double row16_sum(double s) {
+    s += dpp<0x128>(s);   // row_ror:8
+    s += dpp<0x124>(s);   // row_ror:4
+    s += dpp<0x122>(s);   // row_ror:2
+    s += dpp<0x121>(s);   // row_ror:1
+    return s;
+}
+
+// Accumulate CH per-thread values x[0..CH) over the block's 256 rows into
+// acc[base .. base+CH) (LDS).  Fixed order: lane (col*16+part) sums rows q*16+part of
+// column col (q ascending), then a DPP row sum.
 __device__ __forceinline__ void chunk_reduce(const double (&x)[CH], double* __restrict__ tr,
                                              double* __restrict__ acc, int base, bool first) {
     const int t = threadIdx.x;
@@ -58,150 +89,166 @@ __device__ __forceinline__ void chunk_reduce(const double (&x)[CH], double* __re
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) s += tr[col * TSTR + q * 16 + part];
-    s += __shfl_xor(s, 8);
-    s += __shfl_xor(s, 4);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 1);
+    s = row16_sum(s);
     if (part == 0) acc[base + col] = first ? s : acc[base + col] + s;
     __syncthreads();
 }
 
-// Block-reduce one per-thread scalar into acc[base].
-__device__ __forceinline__ void reduce_one(double y, double* tr, double* acc, int base, bool first) {
-    const int t = threadIdx.x;
-    double s = y;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if ((t & 63) == 0) tr[CH * TSTR - 4 + (t >> 6)] = s;
-    __syncthreads();
-    if (t == 0) {
-        const double* w = tr + CH * TSTR - 4;
-        const double tot = (w[0] + w[1]) + (w[2] + w[3]);
-        acc[base] = first ? tot : acc[base] + tot;
-    }
-    __syncthreads();
-}
-
-// The first MAXC columns of this thread's row of V live in VGPRs; columns beyond
-// MAXC (kmax > MAXC) are streamed from memory on each use.
+// Row of V held in VGPRs: v[c] = V[r, c] for c < MAXC (zero for c >= the range the
+// tile resource admits).
 template <int MAXC>
 struct Row {
     double v[MAXC];
-    __device__ __forceinline__ void load(const double* __restrict__ V, int64_t ld, int64_t r,
-                                         int ncols, bool ok) {
+    __device__ __forceinline__ void load(rsrc_t tile, uint32_t toff) {
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) v[c] = (ok && c < ncols) ? V[r + (int64_t)c * ld] : 0.0;
+        for (int c = 0; c < MAXC; ++c) v[c] = bld(tile, toff + (uint32_t)c * (TPB * 8));
     }
 };
 
-// sum_c V[r, c] * h[c], c < ncols (h uniform, in global memory)
+// sum_c V[r,c] * h[c] for c < nc.  h is in LDS (broadcast reads) and zero-padded to
+// MAXC, and R.v[c] is zero for c >= nc (range-checked load): no per-column conditions.
 template <int MAXC>
-__device__ __forceinline__ double row_dot(const Row<MAXC>& R, const double* __restrict__ V,
-                                          int64_t ld, int64_t r, int ncols, bool ok,
+__device__ __forceinline__ double row_dot(const Row<MAXC>& R, rsrc_t tile, uint32_t toff, int nc,
                                           const double* __restrict__ h) {
     double s = 0.0;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-        if (c < ncols) s += R.v[c] * h[c];
-    for (int c = MAXC; c < ncols; ++c) s += (ok ? V[r + (int64_t)c * ld] : 0.0) * h[c];
+    for (int c = 0; c < MAXC; ++c) s += R.v[c] * h[c];
+    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + (uint32_t)c * (TPB * 8)) * h[c];
     return s;
 }
 
-// Block-reduce x_c = V[r, c] * y, c < ncols, into acc[base + c] (acc entries up to
-// base + roundup16(ncols) are written; later reduce_one calls may overwrite them).
+// Block-reduce V[r,i]*y for i < lim (lim == the row's loaded column count, so R.v[i]
+// is zero beyond it) into acc[base .. base+lim).  Entries up to base+roundup16(lim)
+// receive zeros (callers reduce extra scalars into them afterwards).
 template <int MAXC>
-__device__ __forceinline__ void reduce_cols(const Row<MAXC>& R, const double* __restrict__ V,
-                                            int64_t ld, int64_t r, int ncols, bool ok, double y,
-                                            double* tr, double* acc, int base, bool first) {
+__device__ __forceinline__ void reduce_row(const Row<MAXC>& R, rsrc_t tile, uint32_t toff, int lim,
+                                           double y, double* tr, double* acc, int base, bool first) {
 #pragma unroll
     for (int c0 = 0; c0 < MAXC; c0 += CH) {
-        if (c0 < ncols) {
+        if (c0 < lim) {
             double x[CH];
 #pragma unroll
-            for (int q = 0; q < CH; ++q) x[q] = (c0 + q < ncols) ? R.v[c0 + q] * y : 0.0;
+            for (int q = 0; q < CH; ++q) x[q] = R.v[c0 + q] * y;
             chunk_reduce(x, tr, acc, base + c0, first);
         }
     }
-    for (int c0 = MAXC; c0 < ncols; c0 += CH) {
+    for (int c0 = MAXC; c0 < lim; c0 += CH) {
         double x[CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-            const int c = c0 + q;
-            x[q] = (ok && c < ncols) ? V[r + (int64_t)c * ld] * y : 0.0;
-        }
+        for (int q = 0; q < CH; ++q) x[q] = bld(tile, toff + (uint32_t)(c0 + q) * (TPB * 8)) * y;
         chunk_reduce(x, tr, acc, base + c0, first);
     }
 }
 
-// Streaming (no row cache) variant for kernels that touch V only for a Gram row.
-__device__ __forceinline__ void reduce_cols_stream(const double* __restrict__ V, int64_t ld,
-                                                   int64_t r, int ncols, bool ok, double y,
-                                                   double* tr, double* acc, int base, bool first) {
-    for (int c0 = 0; c0 < ncols; c0 += CH) {
+// Same without a register row (streams V[r, 0..lim) from the tile; the tile resource
+// must admit exactly lim columns).
+__device__ __forceinline__ void reduce_stream(rsrc_t tile, uint32_t toff, int lim, double y, double* tr,
+                                              double* acc, int base, bool first) {
+    for (int c0 = 0; c0 < lim; c0 += CH) {
         double x[CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-            const int c = c0 + q;
-            x[q] = (ok && c < ncols) ? V[r + (int64_t)c * ld] * y : 0.0;
-        }
+        for (int q = 0; q < CH; ++q) x[q] = bld(tile, toff + (uint32_t)(c0 + q) * (TPB * 8)) * y;
         chunk_reduce(x, tr, acc, base + c0, first);
     }
 }
 
-__device__ __forceinline__ void zero_acc(double* acc, int lo, int hi) {
-    for (int c = lo + threadIdx.x; c < hi; c += TPB) acc[c] = 0.0;
-}
-
-// Write the block's accumulated values acc[0..nv) to the partial buffer [value][npart].
-__device__ __forceinline__ void store_partials(const double* acc, double* __restrict__ P,
-                                               int npart, int nv) {
+// Block-reduce NE per-thread scalars into acc[base .. base+NE): DPP row sums, then the
+// 16 row totals of each value summed in fixed order by one thread.
+template <int NE>
+__device__ __forceinline__ void reduce_scalars(const double* e, double* tr, double* acc, int base,
+                                               bool first) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const double s = row16_sum(e[k]);
+        if ((t & 15) == 0) tr[k * 16 + (t >> 4)] = s;
+    }
     __syncthreads();
-    for (int c = threadIdx.x; c < nv; c += TPB) P[(int64_t)c * npart + blockIdx.x] = acc[c];
+    if (t < NE) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) s += tr[t * 16 + q];
+        acc[base + t] = first ? s : acc[base + t] + s;
+    }
+    __syncthreads();
+}
+
+// Block partials -> global [value][npart]
+__device__ __forceinline__ void store_partials(const double* acc, double* P, int npart, int nv) {
+    __syncthreads();
+    for (int c = threadIdx.x; c < nv; c += TPB) GP(double, P)[(int64_t)c * npart + blockIdx.x] = acc[c];
+}
+
+// Copy nc coefficients from global to LDS, zero-padded to `pad` entries (caller syncs).
+__device__ __forceinline__ void stage(double* dst, const double* src, int nc, int pad) {
+    const int m = nc > pad ? nc : pad;
+    for (int c = threadIdx.x; c < m; c += TPB) dst[c] = c < nc ? GP(const double, src)[c] : 0.0;
 }
 
 // CSR row sum in ascending column order, products and sums separately rounded.
-__device__ __forceinline__ double spmv_row(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                           const double* __restrict__ val, const double* __restrict__ x,
-                                           int64_t r) {
-#pragma clang fp contract(off)
+__device__ __forceinline__ double spmv_row(const int* rowptr, const int* col, const double* val,
+                                           const double* x, int64_t r) {
     double s = 0.0;
-    const int p1 = rowptr[r + 1];
-    for (int p = rowptr[r]; p < p1; ++p) s = add_rn(s, mul_rn(val[p], x[col[p]]));
+    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
+    for (int p = p0; p < p1; ++p)
+        s = add_rn(s, mul_rn(GP(const double, val)[p], GP(const double, x)[GP(const int, col)[p]]));
     return s;
 }
-// Same, gathering fl(x[c] * scale) -- bitwise the stored Lanczos column -- or zeros.
-__device__ __forceinline__ double spmv_row_scaled(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                                  const double* __restrict__ val, const double* __restrict__ x,
-                                                  double scale, bool zero, int64_t r) {
-#pragma clang fp contract(off)
+// Same, gathering column jc of the tile-major basis (x[c] = V[c, jc]).
+__device__ __forceinline__ double spmv_row_v(const int* rowptr, const int* col, const double* val,
+                                             const double* V, int64_t tstride, int jc, int64_t r) {
     double s = 0.0;
-    const int p1 = rowptr[r + 1];
-    for (int p = rowptr[r]; p < p1; ++p) {
-        const double xv = zero ? 0.0 : mul_rn(x[col[p]], scale);
-        s = add_rn(s, mul_rn(val[p], xv));
+    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
+    for (int p = p0; p < p1; ++p) {
+        const int64_t cidx = GP(const int, col)[p];
+        const double xv = GP(const double, V)[(cidx >> 8) * tstride + (int64_t)jc * TPB + (cidx & 255)];
+        s = add_rn(s, mul_rn(GP(const double, val)[p], xv));
+    }
+    return s;
+}
+// Same, gathering fl(x[c] * scale) (bitwise the stored Lanczos column) or zeros.
+__device__ __forceinline__ double spmv_row_scaled(const int* rowptr, const int* col, const double* val,
+                                                  const double* x, double scale, bool zero, int64_t r) {
+    double s = 0.0;
+    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
+    for (int p = p0; p < p1; ++p) {
+        const double xv = zero ? 0.0 : mul_rn(GP(const double, x)[GP(const int, col)[p]], scale);
+        s = add_rn(s, mul_rn(GP(const double, val)[p], xv));
     }
     return s;
 }
 
-#define KERNEL_PROLOGUE                                   \
-    __shared__ double tr[CH * TSTR];                      \
-    extern __shared__ __attribute__((aligned(16))) double acc[]; \
-    const DFac& d = F[blockIdx.y];
+__device__ __forceinline__ double ld(const double* p, int64_t i) { return GP(const double, p)[i]; }
+__device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, p)[i] = v; }
 
-#define TILE_LOOP                                                                   \
-    bool first = true;                                                              \
-    for (int tile = blockIdx.x; tile < a.ntiles; tile += a.npart, first = false) {  \
-        const int64_t r = (int64_t)tile * TPB + threadIdx.x;                        \
-        const bool ok = r < a.n;
+// Shared prologue: descriptor, LDS, tile loop.  Rows r >= n are padding (all inputs
+// zero there); `ok` guards only the SpMV and the stored scalars.
+#define KERNEL_PROLOGUE                                                \
+    __shared__ double tr[CH * TSTR];                                   \
+    extern __shared__ __attribute__((aligned(16))) double lds[];       \
+    const DFac& d = F[blockIdx.y];                                     \
+    const int64_t TS = (int64_t)TPB * (a.kmax + 1);                    \
+    (void)TS;
+
+#define TILE_LOOP                                                                  \
+    bool first = true;                                                             \
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += a.npart, first = false) { \
+        const int64_t r = (int64_t)tile * TPB + threadIdx.x;                       \
+        const bool ok = r < a.n;                                                   \
+        const double* Vt = d.V + (int64_t)tile * TS;                               \
+        const uint32_t toff = threadIdx.x * 8u;                                    \
+        (void)Vt; (void)toff; (void)ok;
 
 // ------------------------------------------------------------------ init kernels
 
 // P1 = [ sum b^2 ]
 __global__ __launch_bounds__(TPB) void k_init_a(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
+    double* acc = lds;
     TILE_LOOP
-        const double bv = ok ? d.b[r] : 0.0;
-        reduce_one(bv * bv, tr, acc, 0, first);
+        const double bv = ld(d.b, r);
+        const double e[1] = {bv * bv};
+        reduce_scalars<1>(e, tr, acc, 0, first);
     }
     store_partials(acc, d.P1, a.npart, 1);
 }
@@ -210,13 +257,14 @@ __global__ __launch_bounds__(TPB) void k_init_a(const DFac* __restrict__ F, KArg
 __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
-    const double inv = d.sc[SC_INVB];
+    double* acc = lds;
+    const double inv = ld(d.sc, SC_INVB);
     TILE_LOOP
-        const double bv = ok ? d.b[r] : 0.0;
+        const double bv = ld(d.b, r);
         const double v0 = inv * bv;
-        if (ok) d.V[r] = v0;
-        reduce_one(v0 * bv, tr, acc, 0, first);
-        reduce_one(v0 * v0, tr, acc, 1, first);
+        st(d.V, (int64_t)tile * TS + threadIdx.x, v0);
+        const double e[2] = {v0 * bv, v0 * v0};
+        reduce_scalars<2>(e, tr, acc, 0, first);
     }
     store_partials(acc, d.P1, a.npart, 2);
 }
@@ -227,14 +275,15 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
+    double* acc = lds;
     const int j = a.j, nc = j + 1;
-    const double* vj = d.V + (int64_t)j * a.ld;
     TILE_LOOP
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
         Row<MAXC> R;
-        R.load(d.V, a.ld, r, nc, ok);
-        const double w = ok ? spmv_row(d.rowptr, d.col, d.val, vj, r) : 0.0;
-        if (ok) d.W[r] = w;
-        reduce_cols(R, d.V, a.ld, r, nc, ok, w, tr, acc, 0, first);
+        R.load(tv, toff);
+        const double w = ok ? spmv_row_v(d.rowptr, d.col, d.val, d.V, TS, j, r) : 0.0;
+        st(d.W, r, w);
+        reduce_row<MAXC>(R, tv, toff, nc, w, tr, acc, 0, first);
     }
     store_partials(acc, d.P1, a.npart, nc);
 }
@@ -242,36 +291,41 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
 // First pass of step j fused with writing the pending column v_j of step j-1:
 //   v_j = (U - V[:,0..j) h2) * inv_beta                     -> V[:, j]
 //   W   = (A U - V[:,0..j) g[0..j) - g[j] v_j) * inv_beta    (= A v_j, Arnoldi relation)
-//   P1  = [ <V[:,c],W> (c<j), <v_j,W> | gram <V[:,c],v_j> (c<j), <v_j,v_j> | <v_j,b> ]
+//   P1  = [ <V[:,c],W> (c<j), <v_j,W>, <v_j,b> | gram: <V[:,c],v_j> (c<j), <v_j,v_j> ]
 template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j;
-    const double inv_beta = d.sc[SC_INVBETA];
-    const double gj = d.g[j];
+    const int CP = COEF_PAD(a.kmax);
+    double* h2 = lds;                 // [j], zero-padded
+    double* g = lds + CP;             // [j+1], zero-padded (g[j] read separately)
+    double* acc = lds + 2 * CP;
+    stage(h2, d.h2, j, CP);
+    stage(g, d.g, j, CP);
+    __syncthreads();
+    const double inv_beta = ld(d.sc, SC_INVBETA);
+    const double gj = ld(d.g, j);
     const bool gram = d.track_gram != 0;
-    double* vj_out = d.V + (int64_t)j * a.ld;
     TILE_LOOP
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)j * TPB * 8);
         Row<MAXC> R;
-        R.load(d.V, a.ld, r, j, ok);
-        const double up = ok ? d.U[r] : 0.0;
-        const double vj = ok ? (up - row_dot(R, d.V, a.ld, r, j, ok, d.h2)) * inv_beta : 0.0;
+        R.load(tv, toff);
+        const double up = ld(d.U, r);
+        const double vj = ok ? (up - row_dot(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double au = ok ? spmv_row(d.rowptr, d.col, d.val, d.U, r) : 0.0;
-        const double w = ok ? (au - row_dot(R, d.V, a.ld, r, j, ok, d.g) - gj * vj) * inv_beta : 0.0;
-        if (ok) {
-            vj_out[r] = vj;
-            d.W[r] = w;
-        }
-        reduce_cols(R, d.V, a.ld, r, j, ok, w, tr, acc, 0, first);
-        reduce_one(vj * w, tr, acc, j, first);
+        const double w = ok ? (au - row_dot(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
+        st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
+        st(d.W, r, w);
+        reduce_row<MAXC>(R, tv, toff, j, w, tr, acc, 0, first);
+        const double e1[2] = {vj * w, vj * ld(d.b, r)};
+        reduce_scalars<2>(e1, tr, acc, j, first);
         if (gram) {
-            reduce_cols(R, d.V, a.ld, r, j, ok, vj, tr, acc, j + 1, first);
-            reduce_one(vj * vj, tr, acc, 2 * j + 1, first);
+            reduce_row<MAXC>(R, tv, toff, j, vj, tr, acc, j + 2, first);
+            const double e2[1] = {vj * vj};
+            reduce_scalars<1>(e2, tr, acc, 2 * j + 2, first);
         }
-        reduce_one(ok ? vj * d.b[r] : 0.0, tr, acc, 2 * j + 2, first);
     }
-    if (!gram) zero_acc(acc, j + 1, 2 * j + 2);
-    store_partials(acc, d.P1, a.npart, 2 * j + 3);
+    store_partials(acc, d.P1, a.npart, gram ? 2 * j + 3 : j + 2);
 }
 
 // Second pass: U = W - V[:,0..j] h1;  P2 = [ <V[:,c],U> (c<=j), <U,U> ].
@@ -279,14 +333,21 @@ template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
+    const int CP = COEF_PAD(a.kmax);
+    double* h1 = lds;
+    double* acc = lds + CP;
+    stage(h1, d.RED1, nc, CP);
+    __syncthreads();
     TILE_LOOP
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
         Row<MAXC> R;
-        R.load(d.V, a.ld, r, nc, ok);
-        const double w = ok ? d.W[r] : 0.0;
-        const double u = ok ? (w - row_dot(R, d.V, a.ld, r, nc, ok, d.RED1)) : 0.0;
-        if (ok) d.U[r] = u;
-        reduce_cols(R, d.V, a.ld, r, nc, ok, u, tr, acc, 0, first);
-        reduce_one(u * u, tr, acc, nc, first);
+        R.load(tv, toff);
+        const double w = ld(d.W, r);
+        const double u = ok ? (w - row_dot(R, tv, toff, nc, h1)) : 0.0;
+        st(d.U, r, u);
+        reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
+        const double e[1] = {u * u};
+        reduce_scalars<1>(e, tr, acc, nc, first);
     }
     store_partials(acc, d.P2, a.npart, nc + 1);
 }
@@ -297,17 +358,22 @@ template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_finalize(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
-    const double inv_beta = d.sc[SC_INVBETA];
-    double* vout = d.V + (int64_t)(j + 1) * a.ld;
+    const int CP = COEF_PAD(a.kmax);
+    double* h2 = lds;
+    double* acc = lds + CP;
+    stage(h2, d.h2, nc, CP);
+    __syncthreads();
+    const double inv_beta = ld(d.sc, SC_INVBETA);
     TILE_LOOP
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
         Row<MAXC> R;
-        R.load(d.V, a.ld, r, nc, ok);
-        const double up = ok ? d.U[r] : 0.0;
-        const double v = ok ? (up - row_dot(R, d.V, a.ld, r, nc, ok, d.h2)) * inv_beta : 0.0;
-        if (ok) vout[r] = v;
-        reduce_cols(R, d.V, a.ld, r, nc, ok, v, tr, acc, 0, first);
-        reduce_one(v * v, tr, acc, nc, first);
-        reduce_one(ok ? v * d.b[r] : 0.0, tr, acc, nc + 1, first);
+        R.load(tv, toff);
+        const double up = ld(d.U, r);
+        const double v = ok ? (up - row_dot(R, tv, toff, nc, h2)) * inv_beta : 0.0;
+        st(d.V, (int64_t)tile * TS + (int64_t)(j + 1) * TPB + threadIdx.x, v);
+        reduce_row<MAXC>(R, tv, toff, nc, v, tr, acc, 0, first);
+        const double e[2] = {v * v, v * ld(d.b, r)};
+        reduce_scalars<2>(e, tr, acc, nc, first);
     }
     store_partials(acc, d.P1, a.npart, nc + 2);
 }
@@ -319,20 +385,17 @@ __global__ __launch_bounds__(TPB) void k_arn_finalize(const DFac* __restrict__ F
 __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
+    double* acc = lds;
     const int j = a.j;
-    const double* vj = d.V + (int64_t)j * a.ld;
-    const double* vp = d.V + (int64_t)(j > 0 ? j - 1 : 0) * a.ld;
-    const double bp = j > 0 ? d.sc[SC_BETAPREV] : 0.0;
+    const double bp = j > 0 ? ld(d.sc, SC_BETAPREV) : 0.0;
     TILE_LOOP
-        double u = 0.0, v = 0.0;
-        if (ok) {
-            const double av = spmv_row(d.rowptr, d.col, d.val, vj, r);
-            const double prev = j > 0 ? vp[r] : 0.0;
-            u = av - bp * prev;
-            v = vj[r];
-            d.U[r] = u;
-        }
-        reduce_one(u * v, tr, acc, 0, first);
+        const double av = ok ? spmv_row_v(d.rowptr, d.col, d.val, d.V, TS, j, r) : 0.0;
+        const double prev = j > 0 ? ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x) : 0.0;
+        const double u = av - bp * prev;
+        const double v = ld(Vt, (int64_t)j * TPB + threadIdx.x);
+        st(d.U, r, u);
+        const double e[1] = {u * v};
+        reduce_scalars<1>(e, tr, acc, 0, first);
     }
     store_partials(acc, d.P1, a.npart, 1);
 }
@@ -343,48 +406,42 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F
 __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
+    double* acc = lds;
     const int j = a.j;
-    const double beta = d.sc[SC_BETA];
-    const double inv_beta = d.sc[SC_INVBETA];
+    const double beta = ld(d.sc, SC_BETA);
+    const double inv_beta = ld(d.sc, SC_INVBETA);
     const bool zero = (beta == 0.0);
-    const double* vp = d.V + (int64_t)(j - 1) * a.ld;
-    double* vj_out = d.V + (int64_t)j * a.ld;
     const bool gram = d.track_gram != 0;
     TILE_LOOP
-        double u = 0.0, vj = 0.0, bv = 0.0;
-        if (ok) {
-            vj = zero ? 0.0 : mul_rn(d.W[r], inv_beta);
-            const double av = spmv_row_scaled(d.rowptr, d.col, d.val, d.W, inv_beta, zero, r);
-            u = av - beta * vp[r];
-            vj_out[r] = vj;
-            d.U[r] = u;
-            bv = d.b[r];
-        }
-        reduce_one(u * vj, tr, acc, 0, first);
-        reduce_one(vj * bv, tr, acc, 1, first);
+        const double vj = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+        const double av = ok ? spmv_row_scaled(d.rowptr, d.col, d.val, d.W, inv_beta, zero, r) : 0.0;
+        const double u = av - beta * ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x);
+        st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
+        st(d.U, r, u);
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)j * TPB * 8);
+        const double e1[2] = {u * vj, vj * ld(d.b, r)};
+        reduce_scalars<2>(e1, tr, acc, 0, first);
         if (gram) {
-            reduce_cols_stream(d.V, a.ld, r, j, ok, vj, tr, acc, 2, first);
-            reduce_one(vj * vj, tr, acc, 2 + j, first);
+            reduce_stream(tv, toff, j, vj, tr, acc, 2, first);
+            const double e2[1] = {vj * vj};
+            reduce_scalars<1>(e2, tr, acc, 2 + j, first);
         }
     }
-    if (!gram) zero_acc(acc, 2, 3 + j);
-    store_partials(acc, d.P1, a.npart, j + 3);
+    store_partials(acc, d.P1, a.npart, gram ? j + 3 : 2);
 }
 
 // W = U - alpha v_j (src/orthogonal_bases.jl:53);  P2 = [ <W,W> ]
 __global__ __launch_bounds__(TPB) void k_lan_l2(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
+    double* acc = lds;
     const int j = a.j;
-    const double alpha = d.RED1[0];
-    const double* vj = d.V + (int64_t)j * a.ld;
+    const double alpha = ld(d.RED1, 0);
     TILE_LOOP
-        double w = 0.0;
-        if (ok) {
-            w = d.U[r] - alpha * vj[r];
-            d.W[r] = w;
-        }
-        reduce_one(w * w, tr, acc, 0, first);
+        const double w = ok ? ld(d.U, r) - alpha * ld(Vt, (int64_t)j * TPB + threadIdx.x) : 0.0;
+        st(d.W, r, w);
+        const double e[1] = {w * w};
+        reduce_scalars<1>(e, tr, acc, 0, first);
     }
     store_partials(acc, d.P2, a.npart, 1);
 }
@@ -394,135 +451,164 @@ __global__ __launch_bounds__(TPB) void k_lan_l2(const DFac* __restrict__ F, KArg
 __global__ __launch_bounds__(TPB) void k_lan_finalize(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
+    double* acc = lds;
     const int j = a.j, nc = j + 1;
-    const double beta = d.sc[SC_BETA];
-    const double inv_beta = d.sc[SC_INVBETA];
+    const double beta = ld(d.sc, SC_BETA);
+    const double inv_beta = ld(d.sc, SC_INVBETA);
     const bool zero = (beta == 0.0);
-    double* vout = d.V + (int64_t)(j + 1) * a.ld;
     const bool gram = d.track_gram != 0;
     TILE_LOOP
-        double v = 0.0, bv = 0.0;
-        if (ok) {
-            v = zero ? 0.0 : mul_rn(d.W[r], inv_beta);
-            vout[r] = v;
-            bv = d.b[r];
-        }
-        reduce_one(v * bv, tr, acc, 0, first);
+        const double v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+        st(d.V, (int64_t)tile * TS + (int64_t)(j + 1) * TPB + threadIdx.x, v);
+        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
+        const double e1[1] = {v * ld(d.b, r)};
+        reduce_scalars<1>(e1, tr, acc, 0, first);
         if (gram) {
-            reduce_cols_stream(d.V, a.ld, r, nc, ok, v, tr, acc, 1, first);
-            reduce_one(v * v, tr, acc, 1 + nc, first);
+            reduce_stream(tv, toff, nc, v, tr, acc, 1, first);
+            const double e2[1] = {v * v};
+            reduce_scalars<1>(e2, tr, acc, 1 + nc, first);
         }
     }
-    if (!gram) zero_acc(acc, 1, 2 + nc);
-    store_partials(acc, d.P1, a.npart, nc + 2);
+    store_partials(acc, d.P1, a.npart, gram ? nc + 2 : 1);
 }
 
 // ------------------------------------------------------------------ reductions
 
-// RED[c] = sum_b P[c*npart + b]: one wave per value, fixed order.
+// RED[c] = sum_b P[c*npart + b]: one wave per value, fixed order (16 independent
+// strided loads per lane, then a fixed-order combine).
 __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int which, int nv, int npart) {
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
     if (c >= nv) return;
     const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
-    double s = 0.0;
-    for (int b = threadIdx.x; b < npart; b += 64) s += P[b];
+    const int l = threadIdx.x;
+    double part[16];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (threadIdx.x == 0) (which == 1 ? d.RED1 : d.RED2)[c] = s;
+    for (int i = 0; i < 16; ++i) {
+        const int b = l + 64 * i;
+        part[i] = b < npart ? ld(P, b) : 0.0;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += part[i];
+    for (int b = l + 1024; b < npart; b += 64) s += ld(P, b);
+    s = row16_sum(s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (l == 0) st(which == 1 ? d.RED1 : d.RED2, c, s);
 }
 
 // ------------------------------------------------------------------ post-processing
-// One 64-thread block per factor: turns reduced values into H / beta / records.
+// One 256-thread block per local factor: reduced values -> H / beta / records.
+// `clear` zeroes the factor's record row first (the first post of a record slot).
 
 __device__ __forceinline__ void put_gram(double* rec, int kmax, int c, const double* row, double bt,
                                          int tracked) {
     if (tracked)
-        for (int i = threadIdx.x; i <= c; i += 64) rec[rec_gram(kmax) + i] = row[i];
+        for (int i = threadIdx.x; i <= c; i += TPB) st(rec, rec_gram(kmax) + i, ld(row, i));
     if (threadIdx.x == 0) {
-        rec[rec_bt(kmax)] = bt;
-        rec[rec_col(kmax)] = (double)c;
-        rec[rec_tracked(kmax)] = tracked ? 1.0 : 0.0;
+        st(rec, rec_bt(kmax), bt);
+        st(rec, rec_col(kmax), (double)c);
+        st(rec, rec_tracked(kmax), tracked ? 1.0 : 0.0);
     }
 }
 
-__global__ __launch_bounds__(64) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag) {
+__global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag,
+                                              int clear) {
+    __shared__ double sh[TPB];
+    __shared__ double h2s[1024 + 8];
     const DFac& d = F[blockIdx.x];
     const int j = a.j, kmax = a.kmax, KP = kmax + 2;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
     const int t = threadIdx.x;
+    if (clear) {
+        for (int i = t; i < a.m; i += TPB) st(rec, i, 0.0);
+        __syncthreads();
+    }
     if (kind == POST_INIT_A) {
         if (t == 0) {
-            const double nrm = sqrt(d.RED1[0]);
-            d.sc[SC_BNORM] = nrm;
-            d.sc[SC_INVB] = 1.0 / nrm;
+            const double nrm = sqrt(ld(d.RED1, 0));
+            st(d.sc, SC_BNORM, nrm);
+            st(d.sc, SC_INVB, 1.0 / nrm);
         }
         return;
     }
     if (kind == POST_INIT_B) {
-        put_gram(rec, kmax, 0, d.RED1 + 1, d.RED1[0], d.track_gram);
+        put_gram(rec, kmax, 0, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
         return;
     }
     if (kind == POST_ARN) {
-        // RED1 = [h1 (j+1) | gram_j (j+1) | bt_j] (gram/bt only when fused), RED2 = [h2 (j+1) | s]
+        // RED1 = [h1 (j+1) | bt_j | gram_j (j+1)] (bt/gram only when fused); RED2 = [h2 (j+1) | s]
         double* Hc = d.H + (int64_t)j * KP;
-        for (int i = t; i <= j; i += 64) {
-            Hc[i] = d.RED1[i] + d.RED2[i];
-            d.h2[i] = d.RED2[i];
-            rec[i] = Hc[i];
-        }
-        __shared__ double part[64];
         double hh = 0.0;
-        for (int i = t; i <= j; i += 64) hh += d.RED2[i] * d.RED2[i];
-        part[t] = hh;
+        for (int i = t; i <= j; i += TPB) {
+            const double h2 = ld(d.RED2, i);
+            const double hv = ld(d.RED1, i) + h2;
+            st(Hc, i, hv);
+            st(d.h2, i, h2);
+            st(rec, i, hv);
+            if (i < 1024) h2s[i] = h2;
+            hh += h2 * h2;
+        }
+        sh[t] = hh;
         __syncthreads();
         if (t == 0) {
             double s2 = 0.0;
-            for (int i = 0; i < 64; ++i) s2 += part[i];
-            double bsq = d.RED2[j + 1] - s2;
+            for (int i = 0; i < TPB; ++i) s2 += sh[i];
+            const double bsq = ld(d.RED2, j + 1) - s2;
             const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
-            Hc[j + 1] = beta;
-            rec[j + 1] = beta;
-            rec[rec_beta(kmax)] = beta;
-            d.sc[SC_BETA] = beta;
-            d.sc[SC_INVBETA] = 1.0 / beta;
-            d.sc[SC_BETAPREV] = beta;
+            st(Hc, j + 1, beta);
+            st(rec, j + 1, beta);
+            st(rec, rec_beta(kmax), beta);
+            st(d.sc, SC_BETA, beta);
+            st(d.sc, SC_INVBETA, 1.0 / beta);
+            st(d.sc, SC_BETAPREV, beta);
+            sh[0] = beta;
         }
         __syncthreads();
-        // g = Hbar[0..j+1, 0..j] * h2  (column i of Hbar has rows 0..i+1)
-        for (int l = t; l <= j + 1; l += 64) {
+        // g = Hbar[0..j+1, 0..j] * h2 (column i of Hbar has rows 0..i+1); 4 threads per row
+        const int l = t >> 2, part = t & 3;
+        for (int l0 = 0; l0 <= j + 1; l0 += TPB / 4) {
+            const int ll = l0 + l;
             double s = 0.0;
-            for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) s += d.H[(int64_t)i * KP + l] * d.RED2[i];
-            d.g[l] = s;
+            if (ll <= j + 1) {
+                for (int i = (ll > 0 ? ll - 1 : 0) + part; i <= j; i += 4) {
+                    const double hv = (i == j) ? (ll == j + 1 ? sh[0] : ld(Hc, ll)) : ld(d.H, (int64_t)i * KP + ll);
+                    s += hv * (i < 1024 ? h2s[i] : ld(d.h2, i));
+                }
+            }
+            s += __shfl_xor(s, 1);
+            s += __shfl_xor(s, 2);
+            if (part == 0 && ll <= j + 1) st(d.g, ll, s);
         }
-        if (flag) put_gram(rec, kmax, j, d.RED1 + j + 1, d.RED1[2 * j + 2], d.track_gram);
-        else if (t == 0) rec[rec_col(kmax)] = -1.0;
+        if (flag) put_gram(rec, kmax, j, d.RED1 + j + 2, ld(d.RED1, j + 1), d.track_gram);
+        else if (t == 0) st(rec, rec_col(kmax), -1.0);
         return;
     }
     if (kind == POST_ARN_FIN) {
         // RED1 = [gram_{j+1} (j+2) | bt]
-        put_gram(rec, kmax, j + 1, d.RED1, d.RED1[j + 2], d.track_gram);
+        put_gram(rec, kmax, j + 1, d.RED1, ld(d.RED1, j + 2), d.track_gram);
         return;
     }
     if (kind == POST_LAN) {
         // RED1 = [alpha | bt_j | gram_j (j+1)] (bt/gram only when fused), RED2 = [|w|^2]
         if (t == 0) {
-            const double alpha = d.RED1[0];
-            const double beta = sqrt(d.RED2[0]);
-            rec[j] = alpha;
-            rec[j + 1] = beta;
-            rec[rec_beta(kmax)] = beta;
-            d.sc[SC_BETA] = beta;
-            d.sc[SC_INVBETA] = 1.0 / beta;
-            d.sc[SC_BETAPREV] = beta;
+            const double alpha = ld(d.RED1, 0);
+            const double beta = sqrt(ld(d.RED2, 0));
+            st(rec, j, alpha);
+            st(rec, j + 1, beta);
+            st(rec, rec_beta(kmax), beta);
+            st(d.sc, SC_BETA, beta);
+            st(d.sc, SC_INVBETA, 1.0 / beta);
+            st(d.sc, SC_BETAPREV, beta);
         }
-        if (flag) put_gram(rec, kmax, j, d.RED1 + 2, d.RED1[1], d.track_gram);
-        else if (t == 0) rec[rec_col(kmax)] = -1.0;
+        if (flag) put_gram(rec, kmax, j, d.RED1 + 2, ld(d.RED1, 1), d.track_gram);
+        else if (t == 0) st(rec, rec_col(kmax), -1.0);
         return;
     }
     if (kind == POST_LAN_FIN) {
         // RED1 = [bt | gram_{j+1} (j+2)]
-        put_gram(rec, kmax, j + 1, d.RED1 + 1, d.RED1[0], d.track_gram);
+        put_gram(rec, kmax, j + 1, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
         return;
     }
 }
@@ -531,52 +617,58 @@ __global__ __launch_bounds__(64) void k_post(const DFac* __restrict__ F, KArgs a
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-// X[:, t0..t0+64) = V[:, 0..k) * Y[:, t0..t0+64) for one factor (blockIdx.y), Y
-// column-major k x t.  Each wave computes 16-row strips for up to four 16-column
-// tiles with v_mfma_f64_16x16x4_f64:
-//   A = V[16 rows x 4 cols]  lane l: row l&15, col l>>4   (coalesced 128 B per column)
-//   B = Y[4 x 16]            lane l: row l>>4, col l&15   (from LDS)
+// X[:, t0..t0+16*NG) = V[:, 0..k) * Y[:, t0..) (Y column-major k x t) for factor
+// blockIdx.y; X column-major with leading dimension ld.  Block = one 256-row tile;
+// wave w owns rows 64w..64w+63 as 4 strips of 16; NG 16-column groups per launch
+// (blockIdx.z walks further groups).  v_mfma_f64_16x16x4_f64 with
+//   A = V[16 rows x 4 cols]  lane l: row l&15, col l>>4 (tile buffer load, range-checked)
+//   B = Y[4 x 16]            lane l: row l>>4, col l&15 (LDS)
 //   D                        lane l: row (l>>4) + 4i, col l&15
-// k is walked in chunks of 64 staged through LDS.
+// Each D register store covers 4 consecutive rows of 16 columns; the four registers
+// of a strip complete 16-row runs that the L2 merges before write-back.
+template <int NG>
 __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
                                                    const double* __restrict__ Yall,
                                                    double* __restrict__ Xall, int k, int t) {
-    __shared__ double Ys[64 * 65];   // [col][kk] padded
+    __shared__ double Ys[64 * 80];   // [kk][col] of one 64-deep k chunk (stride 80: conflict-free)
     const int f = blockIdx.y;
     const DFac& d = F[f];
+    const int64_t TS = (int64_t)TPB * (a.kmax + 1);
     const double* Y = Yall + (int64_t)f * k * t;
     double* X = Xall + (int64_t)f * a.ld * t;
-    const int t0 = blockIdx.z * 64;
-    const int tn = min(64, t - t0);
+    const int tile = blockIdx.x;
+    const double* Vt = d.V + (int64_t)tile * TS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
-    f64x4 acc[4][4];
+    const int t0 = blockIdx.z * 16 * NG;
+    const int tn = min(16 * NG, t - t0);
+    f64x4 acc[4][NG];
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[s][q] = (f64x4){0.0, 0.0, 0.0, 0.0};
-    const int64_t rb = (int64_t)blockIdx.x * 256 + wave * 64;
+        for (int q = 0; q < NG; ++q) acc[s][q] = (f64x4){0.0, 0.0, 0.0, 0.0};
     for (int k0 = 0; k0 < k; k0 += 64) {
         const int kn = min(64, k - k0);
         __syncthreads();
-        for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+        for (int i = threadIdx.x; i < 64 * 16 * NG; i += 256) {
             const int kk = i & 63, tt = i >> 6;
-            Ys[tt * 65 + kk] = (kk < kn && tt < tn) ? Y[(int64_t)(t0 + tt) * k + k0 + kk] : 0.0;
+            Ys[kk * 80 + tt] = (kk < kn && tt < tn) ? ld(Y, (int64_t)(t0 + tt) * k + k0 + kk) : 0.0;
         }
         __syncthreads();
+        const rsrc_t tv = mkrsrc(Vt + (int64_t)k0 * TPB, (uint32_t)kn * TPB * 8);
         const int kp = (kn + 3) & ~3;
         for (int kk = 0; kk < kp; kk += 4) {
             const int ka = kk + lk;
-            double b0 = Ys[(0 + lr) * 65 + ka], b1 = Ys[(16 + lr) * 65 + ka];
-            double b2 = Ys[(32 + lr) * 65 + ka], b3 = Ys[(48 + lr) * 65 + ka];
+            double bq[NG];
+#pragma unroll
+            for (int q = 0; q < NG; ++q) bq[q] = Ys[ka * 80 + 16 * q + lr];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const int64_t ra = rb + s * 16 + lr;
-                const double av = (ra < a.n && ka < kn) ? d.V[ra + (int64_t)(k0 + ka) * a.ld] : 0.0;
-                acc[s][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc[s][0], 0, 0, 0);
-                if (tn > 16) acc[s][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc[s][1], 0, 0, 0);
-                if (tn > 32) acc[s][2] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b2, acc[s][2], 0, 0, 0);
-                if (tn > 48) acc[s][3] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b3, acc[s][3], 0, 0, 0);
+                const int row = wave * 64 + s * 16 + lr;
+                const double av = bld(tv, (uint32_t)(ka * TPB + row) * 8u);
+#pragma unroll
+                for (int q = 0; q < NG; ++q)
+                    acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bq[q], acc[s][q], 0, 0, 0);
             }
         }
     }
@@ -584,12 +676,12 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int64_t rr = rb + s * 16 + lk + 4 * i;
+            const int64_t rr = (int64_t)tile * TPB + wave * 64 + s * 16 + lk + 4 * i;
             if (rr < a.n) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < NG; ++q) {
                     const int c = q * 16 + lr;
-                    if (c < tn) X[rr + (int64_t)(t0 + c) * a.ld] = acc[s][q][i];
+                    if (c < tn) st(X, rr + (int64_t)(t0 + c) * a.ld, acc[s][q][i]);
                 }
             }
         }
@@ -601,12 +693,24 @@ __global__ __launch_bounds__(TPB) void k_spmv(const int* __restrict__ rowptr, co
                                               const double* __restrict__ val, const double* __restrict__ x,
                                               double* __restrict__ y, int64_t n) {
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (r < n) y[r] = spmv_row(rowptr, col, val, x, r);
+    if (r < n) st(y, r, spmv_row(rowptr, col, val, x, r));
+}
+
+// ------------------------------------------------------------------ tile-major gather/scatter
+// out[c*n + r] = V[r, c0 + c] for one factor (column extraction for the ABI)
+__global__ __launch_bounds__(TPB) void k_get_cols(const double* __restrict__ V, int64_t n, int kmax,
+                                                  int c0, int nc, double* __restrict__ out) {
+    const int64_t TS = (int64_t)TPB * (kmax + 1);
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    const int c = blockIdx.y;
+    if (r < n && c < nc) st(out, (int64_t)c * n + r, ld(V, (r >> 8) * TS + (int64_t)(c0 + c) * TPB + (r & 255)));
 }
 
 // ------------------------------------------------------------------ launchers
 
-static size_t acc_bytes(int nv) { return (size_t)((nv + 32 + 15) & ~15) * sizeof(double); }
+static size_t lds_bytes(int nv, int kmax, int ncoef) {
+    return (size_t)(ncoef * COEF_PAD(kmax) + ((nv + 32 + 15) & ~15)) * sizeof(double);
+}
 
 #define DISPATCH_MAXC(ncols, KERNEL, ...)                  \
     do {                                                   \
@@ -621,51 +725,57 @@ static size_t acc_bytes(int nv) { return (size_t)((nv + 32 + 15) & ~15) * sizeof
     } while (0)
 
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_init_a, dim3(a.npart, nf), dim3(TPB), acc_bytes(1), s, F, a);
+    hipLaunchKernelGGL(k_init_a, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_init_b, dim3(a.npart, nf), dim3(TPB), acc_bytes(2), s, F, a);
+    hipLaunchKernelGGL(k_init_b, dim3(a.npart, nf), dim3(TPB), lds_bytes(2, a.kmax, 0), s, F, a);
 }
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), acc_bytes(a.j + 1), s, F, a);
+    DISPATCH_MAXC(a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 0), s, F, a);
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), acc_bytes(2 * a.j + 3), s, F, a);
+    DISPATCH_MAXC(a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(2 * a.j + 3, a.kmax, 2), s, F, a);
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), acc_bytes(a.j + 2), s, F, a);
+    DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 2, a.kmax, 1), s, F, a);
 }
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_finalize, dim3(a.npart, nf), dim3(TPB), acc_bytes(a.j + 3), s, F, a);
+    DISPATCH_MAXC(a.j + 1, k_arn_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 1), s, F, a);
 }
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_l1_plain, dim3(a.npart, nf), dim3(TPB), acc_bytes(1), s, F, a);
+    hipLaunchKernelGGL(k_lan_l1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_l1_fused, dim3(a.npart, nf), dim3(TPB), acc_bytes(a.j + 3), s, F, a);
+    hipLaunchKernelGGL(k_lan_l1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), acc_bytes(1), s, F, a);
+    hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), acc_bytes(a.j + 3), s, F, a);
+    hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart);
 }
-void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, hipStream_t s) {
-    hipLaunchKernelGGL(k_post, dim3(nf), dim3(64), 0, s, F, a, kind, flag);
+void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
+    hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), 0, s, F, a, kind, flag, clear);
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s) {
-    const int nb = (int)((a.n + 255) / 256);
-    const int nz = (t + 63) / 64;
-    hipLaunchKernelGGL(k_basis_mul, dim3(nb, nf, nz), dim3(256), 0, s, F, a, Y, X, k, t);
+    // NG = 16-column groups per block: t <= 16 -> 1, <= 32 -> 2, else 2 per z-slice
+    if (t <= 16)
+        hipLaunchKernelGGL(k_basis_mul<1>, dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t);
+    else
+        hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
 }
 void launch_spmv(const int* rowptr, const int* col, const double* val, const double* x, double* y,
                  int64_t n, hipStream_t s) {
     const int nb = (int)((n + TPB - 1) / TPB);
     hipLaunchKernelGGL(k_spmv, dim3(nb), dim3(TPB), 0, s, rowptr, col, val, x, y, n);
+}
+void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s) {
+    const int nb = (int)((n + TPB - 1) / TPB);
+    hipLaunchKernelGGL(k_get_cols, dim3(nb, nc), dim3(TPB), 0, s, V, n, kmax, c0, nc, out);
 }
 
 }  // namespace tk

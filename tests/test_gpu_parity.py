@@ -132,22 +132,33 @@ def test_lanczos_matches_oracle(ctx, cls, n, K):
 def test_lanczos_reorth_matches_oracle(ctx):
     """TTR + loss check + MGS redo (src/orthogonal_bases.jl:98-139).  A diagonal matrix
     with geometrically spread eigenvalues makes Ritz values converge fast, so the
-    reference's sqrt(eps) loss check fires repeatedly (11 redo steps in 60)."""
+    sqrt(eps) loss check fires repeatedly.  The loss of orthogonality is itself
+    rounding noise, so near the threshold the decision may differ between any two
+    implementations (the survey found 2-3x between the reference and a restatement);
+    the test therefore (1) checks each device decision against the device's own loss,
+    (2) checks that loss against the loss of the device's V computed here, (3) drives
+    the oracle with the device's decisions and compares H and V, and (4) requires the
+    free-running oracle to agree wherever its loss is not within 2x of sqrt(eps)."""
+    import math
     tk = _tk()
     n, K = 300, 60
+    thr = math.sqrt(np.finfo(float).eps)
     csc = O.dense_to_csc(np.diag(np.geomspace(1.0, 1e6, n)))
     bs = _rhs(n, 1, 3)
     recs, V = _run_device(ctx, tk._lib.TK_LANCZOS_REORTH, csc, bs, K)
     lay = tk._lib.RecordLayout(K)
-    fo = O.Factor(csc, bs[0], K)
-    flags_ref = []
-    for j in range(1, K + 1):
-        _, re = fo.lanczos_reorth(j)
-        flags_ref.append(re)
     flags = [bool(recs[j + 1][0, lay.flag]) for j in range(K)]
-    assert flags == flags_ref
+    losses = np.array([recs[j + 1][0, lay.loss] for j in range(K)])
     assert sum(flags) >= 5
-    # host mirror of H (reference bookkeeping) vs oracle
+    assert all(f == (l > thr) for f, l in zip(flags, losses))
+    # (3) oracle following the device's decisions
+    fo = O.Factor(csc, bs[0], K)
+    for j in range(1, K + 1):
+        lo, _ = fo.lanczos_reorth(j, force=flags[j - 1])
+        if not flags[j - 1] and lo > 1e-11:
+            # (2) loss of the device's TTR vectors ~ the oracle's (same decisions so far);
+            # below ~1e-11 both are rounding noise and only the order of magnitude holds
+            assert lo / 3 < losses[j - 1] < 3 * lo
     td = tk.TensorLanczosReorth.__new__(tk.TensorLanczosReorth)
     tk.TensorDecomposition.__init__(td, tk.KroneckerMatrix(tk.SymInstance, [csc]), K)
     for j in range(K):
@@ -155,6 +166,13 @@ def test_lanczos_reorth_matches_oracle(ctx):
     scale = np.abs(fo.H[:K + 1, :K]).max()
     assert np.abs(td.H[0, :K + 1, :K] - fo.H[:K + 1, :K]).max() <= 1e-10 * scale
     assert np.abs(V[0] - fo.V[:, :K + 1]).max() <= 1e-8
+    # (4) free-running oracle: same decisions away from the threshold band
+    ff = O.Factor(csc, bs[0], K)
+    for j in range(1, K + 1):
+        lo, re = ff.lanczos_reorth(j)
+        if re != flags[j - 1]:
+            assert thr / 2 < lo < 2 * thr, (j, lo)
+            break
 
 
 # ------------------------------------------------------------------ driver vs golden / oracle
