@@ -195,7 +195,64 @@ struct tk_mat {
     int* rowptr = nullptr;
     int* col = nullptr;
     double* val = nullptr;
+    int* doff = nullptr;
+    double* dval = nullptr;
+    int ndiag = 0;
+    int64_t dld = 0;
+    SpM spm() const {
+        SpM m;
+        m.rowptr = rowptr;
+        m.col = col;
+        m.val = val;
+        m.doff = doff;
+        m.dval = dval;
+        m.ndiag = ndiag;
+        m.dld = dld;
+        m.n = n;
+        return m;
+    }
 };
+
+static void free_mat(tk_mat* A) {
+    hipFree(A->rowptr);
+    hipFree(A->col);
+    hipFree(A->val);
+    hipFree(A->doff);
+    hipFree(A->dval);
+    delete A;
+}
+
+// DIA when the matrix is banded with at most TK_MAX_DIAG diagonals that are at least
+// 3/4 full (Laplace: 3, ConvDiff: 4); TKHIP_FORCE_CSR=1 disables it.
+#define TK_MAX_DIAG 8
+static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
+                      const std::vector<double>& v, std::vector<int>& offs, std::vector<double>& dv,
+                      int64_t& dld) {
+    offs.clear();
+    const char* env = getenv("TKHIP_FORCE_CSR");
+    if (env && env[0] == '1') return;
+    std::vector<int> seen;
+    for (int64_t r = 0; r < n; ++r)
+        for (int p = rp[r]; p < rp[r + 1]; ++p) {
+            const int o = ci[p] - (int)r;
+            if (std::find(seen.begin(), seen.end(), o) == seen.end()) {
+                seen.push_back(o);
+                if ((int)seen.size() > TK_MAX_DIAG) return;
+            }
+        }
+    std::sort(seen.begin(), seen.end());
+    const int64_t nd = (int64_t)seen.size();
+    if (nd == 0 || (int64_t)ci.size() * 4 < nd * n * 3) return;
+    dld = (n + 255) / 256 * 256;
+    dv.assign((size_t)nd * dld, 0.0);
+    for (int64_t r = 0; r < n; ++r)
+        for (int p = rp[r]; p < rp[r + 1]; ++p) {
+            const int o = ci[p] - (int)r;
+            const int q = (int)(std::lower_bound(seen.begin(), seen.end(), o) - seen.begin());
+            dv[(size_t)q * dld + r] = v[p];
+        }
+    offs = seen;
+}
 
 static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
                             const std::vector<double>& v, tk_mat** out) {
@@ -203,6 +260,9 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
     A->ctx = c;
     A->n = n;
     A->nnz = (int64_t)ci.size();
+    std::vector<int> offs;
+    std::vector<double> dv;
+    build_dia(n, rp, ci, v, offs, dv, A->dld);
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipMalloc(&A->rowptr, (n + 1) * sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&A->col, std::max<int64_t>(A->nnz, 1) * sizeof(int));
@@ -210,11 +270,15 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
     if (e == hipSuccess) e = hipMemcpy(A->rowptr, rp.data(), (n + 1) * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess && A->nnz) e = hipMemcpy(A->col, ci.data(), A->nnz * sizeof(int), hipMemcpyHostToDevice);
     if (e == hipSuccess && A->nnz) e = hipMemcpy(A->val, v.data(), A->nnz * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !offs.empty()) {
+        A->ndiag = (int)offs.size();
+        e = hipMalloc(&A->doff, offs.size() * sizeof(int));
+        if (e == hipSuccess) e = hipMalloc(&A->dval, dv.size() * sizeof(double));
+        if (e == hipSuccess) e = hipMemcpy(A->doff, offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(A->dval, dv.data(), dv.size() * sizeof(double), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
-        hipFree(A->rowptr);
-        hipFree(A->col);
-        hipFree(A->val);
-        delete A;
+        free_mat(A);
         return fail(TK_ERR_ALLOC, "matrix upload: %s", hipGetErrorString(e));
     }
     *out = A;
@@ -278,12 +342,11 @@ tk_status tk_matrix_from_csr(tk_ctx* c, int64_t n, const int64_t* rowptr, const 
 tk_status tk_matrix_destroy(tk_mat* A) {
     if (!A) return TK_OK;
     hipSetDevice(A->ctx->device);
-    hipFree(A->rowptr);
-    hipFree(A->col);
-    hipFree(A->val);
-    delete A;
+    free_mat(A);
     return TK_OK;
 }
+
+int tk_matrix_format(tk_mat* A) { return A ? A->ndiag : -1; }
 
 tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
     CHECKARG(A && x && y, "NULL argument");
@@ -294,7 +357,7 @@ tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
     hipError_t e = hipMalloc(&dy, A->n * sizeof(double));
     if (e == hipSuccess) e = hipMemcpyAsync(dx, x, A->n * sizeof(double), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
-        launch_spmv(A->rowptr, A->col, A->val, dx, dy, A->n, c->stream);
+        launch_spmv(A->spm(), dx, dy, c->stream);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(y, dy, A->n * sizeof(double), hipMemcpyDeviceToHost, c->stream);
@@ -388,9 +451,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     } while (0)
     for (int f = 0; f < nf; ++f) {
         DFac& d = dc->hf[f];
-        d.rowptr = mats[f]->rowptr;
-        d.col = mats[f]->col;
-        d.val = mats[f]->val;
+        d.A = mats[f]->spm();
         DA(d.V, (size_t)dc->ntiles * 256 * KC * sizeof(double));   // tile-major
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
@@ -550,13 +611,13 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         const bool fused = dc->pending;
         if (fused) {
             RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");
-            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2 * j + 3, dc->npart, s), "reduce");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         } else {
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");
             RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         }
         RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, j + 2, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
@@ -612,7 +673,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dsub, ns, a, s), "arn_a1_plain");
             RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 1, dc->npart, s), "reduce");
             RUN(TCLS_PASS2, 2, launch_arn_a2(dsub, ns, a, s), "arn_a2");
-            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 2, j + 2, dc->npart, s), "reduce");
+            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 2, 2 * j + 4, dc->npart, s), "reduce");
             RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN, 0, 1, s), "post");
             RUN(TCLS_FIN, 2, launch_arn_finalize(dsub, ns, a, s), "arn_finalize");
             RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 3, dc->npart, s), "reduce");

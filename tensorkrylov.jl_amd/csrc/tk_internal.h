@@ -17,12 +17,24 @@ enum {
     SC_COUNT = 8
 };
 
+// Sparse A_s on the device: CSR always; DIA (diagonal storage, ascending offsets,
+// zero-padded) in addition when the matrix is banded with few, mostly full diagonals --
+// then the SpMV has no index loads.  Both sum each row in ascending column order.
+struct SpM {
+    const int* rowptr;    // CSR (n+1)
+    const int* col;       // (nnz) ascending within a row
+    const double* val;    // (nnz)
+    const int* doff;      // DIA offsets (ndiag), ascending
+    const double* dval;   // DIA values [ndiag][dld]: dval[q*dld + r] = A[r, r + doff[q]]
+    int ndiag;            // 0 = CSR only
+    int64_t dld;
+    int64_t n;
+};
+
 // Per-factor device descriptor.  One array of these lives in device memory; kernels
 // index it with blockIdx.y, so every launch covers all of this rank's factors.
 struct DFac {
-    const int* rowptr;    // CSR of A_s (n+1)
-    const int* col;       // (nnz) ascending within a row
-    const double* val;    // (nnz)
+    SpM A;                // A_s
     double* V;            // basis, tile-major: (r/256)*256*(kmax+1) + c*256 + r%256
     const double* b;      // b_s (n)
     double* W;            // work vector (SpMV output / Lanczos v)
@@ -75,8 +87,7 @@ void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int 
 void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s);
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s);
-void launch_spmv(const int* rowptr, const int* col, const double* val, const double* x, double* y,
-                 int64_t n, hipStream_t s);
+void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s);
 
 // record field offsets (see include/tk.h)
 __host__ __device__ inline int rec_len(int kmax) { return 2 * kmax + 10; }

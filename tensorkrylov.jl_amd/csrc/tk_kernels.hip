@@ -185,41 +185,28 @@ __device__ __forceinline__ void stage(double* dst, const double* src, int nc, in
     for (int c = threadIdx.x; c < m; c += TPB) dst[c] = c < nc ? GP(const double, src)[c] : 0.0;
 }
 
-// CSR row sum in ascending column order, products and sums separately rounded.
-__device__ __forceinline__ double spmv_row(const int* rowptr, const int* col, const double* val,
-                                           const double* x, int64_t r) {
+__device__ __forceinline__ double ld(const double* p, int64_t i) { return GP(const double, p)[i]; }
+__device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, p)[i] = v; }
+
+// y[r] = sum over row r of A, terms in ascending column order, products and sums
+// separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
+template <class XF>
+__device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
+#pragma clang fp contract(off)
     double s = 0.0;
-    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
-    for (int p = p0; p < p1; ++p)
-        s = add_rn(s, mul_rn(GP(const double, val)[p], GP(const double, x)[GP(const int, col)[p]]));
-    return s;
-}
-// Same, gathering column jc of the tile-major basis (x[c] = V[c, jc]).
-__device__ __forceinline__ double spmv_row_v(const int* rowptr, const int* col, const double* val,
-                                             const double* V, int64_t tstride, int jc, int64_t r) {
-    double s = 0.0;
-    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
-    for (int p = p0; p < p1; ++p) {
-        const int64_t cidx = GP(const int, col)[p];
-        const double xv = GP(const double, V)[(cidx >> 8) * tstride + (int64_t)jc * TPB + (cidx & 255)];
-        s = add_rn(s, mul_rn(GP(const double, val)[p], xv));
-    }
-    return s;
-}
-// Same, gathering fl(x[c] * scale) (bitwise the stored Lanczos column) or zeros.
-__device__ __forceinline__ double spmv_row_scaled(const int* rowptr, const int* col, const double* val,
-                                                  const double* x, double scale, bool zero, int64_t r) {
-    double s = 0.0;
-    const int p0 = GP(const int, rowptr)[r], p1 = GP(const int, rowptr)[r + 1];
-    for (int p = p0; p < p1; ++p) {
-        const double xv = zero ? 0.0 : mul_rn(GP(const double, x)[GP(const int, col)[p]], scale);
-        s = add_rn(s, mul_rn(GP(const double, val)[p], xv));
+    if (A.ndiag > 0) {
+        for (int q = 0; q < A.ndiag; ++q) {
+            const int64_t c = r + GP(const int, A.doff)[q];
+            const double v = ld(A.dval, (int64_t)q * A.dld + r);
+            if (c >= 0 && c < A.n) s = add_rn(s, mul_rn(v, x(c)));
+        }
+    } else {
+        const int p0 = GP(const int, A.rowptr)[r], p1 = GP(const int, A.rowptr)[r + 1];
+        for (int p = p0; p < p1; ++p) s = add_rn(s, mul_rn(ld(A.val, p), x((int64_t)GP(const int, A.col)[p])));
     }
     return s;
 }
 
-__device__ __forceinline__ double ld(const double* p, int64_t i) { return GP(const double, p)[i]; }
-__device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, p)[i] = v; }
 
 // Shared prologue: descriptor, LDS, tile loop.  Rows r >= n are padding (all inputs
 // zero there); `ok` guards only the SpMV and the stored scalars.
@@ -281,7 +268,8 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
         const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
         Row<MAXC> R;
         R.load(tv, toff);
-        const double w = ok ? spmv_row_v(d.rowptr, d.col, d.val, d.V, TS, j, r) : 0.0;
+        const double* Vg = d.V;
+        const double w = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, nc, w, tr, acc, 0, first);
     }
@@ -291,44 +279,41 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
 // First pass of step j fused with writing the pending column v_j of step j-1:
 //   v_j = (U - V[:,0..j) h2) * inv_beta                     -> V[:, j]
 //   W   = (A U - V[:,0..j) g[0..j) - g[j] v_j) * inv_beta    (= A v_j, Arnoldi relation)
-//   P1  = [ <V[:,c],W> (c<j), <v_j,W>, <v_j,b> | gram: <V[:,c],v_j> (c<j), <v_j,v_j> ]
+//   P1  = [ <V[:,c],W> (c<j), <v_j,W> ]
 template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j;
     const int CP = COEF_PAD(a.kmax);
     double* h2 = lds;                 // [j], zero-padded
-    double* g = lds + CP;             // [j+1], zero-padded (g[j] read separately)
+    double* g = lds + CP;             // [j], zero-padded (g[j] read separately)
     double* acc = lds + 2 * CP;
     stage(h2, d.h2, j, CP);
     stage(g, d.g, j, CP);
     __syncthreads();
     const double inv_beta = ld(d.sc, SC_INVBETA);
     const double gj = ld(d.g, j);
-    const bool gram = d.track_gram != 0;
     TILE_LOOP
         const rsrc_t tv = mkrsrc(Vt, (uint32_t)j * TPB * 8);
         Row<MAXC> R;
         R.load(tv, toff);
+        const double* Ug = d.U;
+        const double au = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot(R, tv, toff, j, h2)) * inv_beta : 0.0;
-        const double au = ok ? spmv_row(d.rowptr, d.col, d.val, d.U, r) : 0.0;
         const double w = ok ? (au - row_dot(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
         st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, j, w, tr, acc, 0, first);
-        const double e1[2] = {vj * w, vj * ld(d.b, r)};
-        reduce_scalars<2>(e1, tr, acc, j, first);
-        if (gram) {
-            reduce_row<MAXC>(R, tv, toff, j, vj, tr, acc, j + 2, first);
-            const double e2[1] = {vj * vj};
-            reduce_scalars<1>(e2, tr, acc, 2 * j + 2, first);
-        }
+        const double e1[1] = {vj * w};
+        reduce_scalars<1>(e1, tr, acc, j, first);
     }
-    store_partials(acc, d.P1, a.npart, gram ? 2 * j + 3 : j + 2);
+    store_partials(acc, d.P1, a.npart, j + 1);
 }
 
-// Second pass: U = W - V[:,0..j] h1;  P2 = [ <V[:,c],U> (c<=j), <U,U> ].
+// Second pass: U = W - V[:,0..j] h1, plus update_rhs! and the Gram row of column j
+// (both need only V[r, 0..j], already in registers):
+//   P2 = [ <V[:,c],U> (c<=j), <U,U>, <v_j,b> | gram <V[:,c],v_j> (c<=j) ]
 template <int MAXC>
 __global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
@@ -338,18 +323,21 @@ __global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArg
     double* acc = lds + CP;
     stage(h1, d.RED1, nc, CP);
     __syncthreads();
+    const bool gram = d.track_gram != 0;
     TILE_LOOP
         const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
         Row<MAXC> R;
         R.load(tv, toff);
+        const double vj = bld(tv, toff + (uint32_t)j * (TPB * 8));
         const double w = ld(d.W, r);
         const double u = ok ? (w - row_dot(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
         reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
-        const double e[1] = {u * u};
-        reduce_scalars<1>(e, tr, acc, nc, first);
+        const double e[2] = {u * u, vj * ld(d.b, r)};
+        reduce_scalars<2>(e, tr, acc, nc, first);
+        if (gram) reduce_row<MAXC>(R, tv, toff, nc, vj, tr, acc, nc + 2, first);
     }
-    store_partials(acc, d.P2, a.npart, nc + 1);
+    store_partials(acc, d.P2, a.npart, gram ? 2 * nc + 2 : nc + 2);
 }
 
 // Write the pending column j+1 with no following step:
@@ -389,7 +377,8 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F
     const int j = a.j;
     const double bp = j > 0 ? ld(d.sc, SC_BETAPREV) : 0.0;
     TILE_LOOP
-        const double av = ok ? spmv_row_v(d.rowptr, d.col, d.val, d.V, TS, j, r) : 0.0;
+        const double* Vg = d.V;
+        const double av = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
         const double prev = j > 0 ? ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x) : 0.0;
         const double u = av - bp * prev;
         const double v = ld(Vt, (int64_t)j * TPB + threadIdx.x);
@@ -414,7 +403,8 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F
     const bool gram = d.track_gram != 0;
     TILE_LOOP
         const double vj = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
-        const double av = ok ? spmv_row_scaled(d.rowptr, d.col, d.val, d.W, inv_beta, zero, r) : 0.0;
+        const double* Wg = d.W;
+        const double av = ok ? spmv(d.A, r, [=](int64_t c) { return zero ? 0.0 : mul_rn(ld(Wg, c), inv_beta); }) : 0.0;
         const double u = av - beta * ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x);
         st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
         st(d.U, r, u);
@@ -513,10 +503,12 @@ __device__ __forceinline__ void put_gram(double* rec, int kmax, int c, const dou
     }
 }
 
+#define POST_LDS_MAX 8192   // doubles of dynamic LDS for Hbar in k_post (kmax <= 88)
 __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag,
                                               int clear) {
-    __shared__ double sh[TPB];
+    __shared__ double sh[16];
     __shared__ double h2s[1024 + 8];
+    extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
     const int j = a.j, kmax = a.kmax, KP = kmax + 2;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
@@ -538,8 +530,10 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         return;
     }
     if (kind == POST_ARN) {
-        // RED1 = [h1 (j+1) | bt_j | gram_j (j+1)] (bt/gram only when fused); RED2 = [h2 (j+1) | s]
+        // RED1 = [h1 (j+1)];  RED2 = [h2 (j+1) | s | bt_j | gram_j (j+1)]
         double* Hc = d.H + (int64_t)j * KP;
+        const int J2 = j + 2;
+        double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // Hbar [i][l]
         double hh = 0.0;
         for (int i = t; i <= j; i += TPB) {
             const double h2 = ld(d.RED2, i);
@@ -547,42 +541,45 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
             st(Hc, i, hv);
             st(d.h2, i, h2);
             st(rec, i, hv);
-            if (i < 1024) h2s[i] = h2;
+            h2s[i] = h2;
+            if (Hs) Hs[j * J2 + i] = hv;
             hh += h2 * h2;
         }
-        sh[t] = hh;
+        if (Hs)
+            for (int idx = t; idx < j * J2; idx += TPB) {
+                const int i = idx / J2, l = idx - i * J2;
+                Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+            }
+        hh = row16_sum(hh);
+        hh += __shfl_xor(hh, 16);
+        hh += __shfl_xor(hh, 32);
+        if ((t & 63) == 0) sh[t >> 6] = hh;
         __syncthreads();
         if (t == 0) {
-            double s2 = 0.0;
-            for (int i = 0; i < TPB; ++i) s2 += sh[i];
+            const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
             const double bsq = ld(d.RED2, j + 1) - s2;
             const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
             st(Hc, j + 1, beta);
+            if (Hs) Hs[j * J2 + j + 1] = beta;
             st(rec, j + 1, beta);
             st(rec, rec_beta(kmax), beta);
             st(d.sc, SC_BETA, beta);
             st(d.sc, SC_INVBETA, 1.0 / beta);
             st(d.sc, SC_BETAPREV, beta);
-            sh[0] = beta;
+            sh[8] = beta;
         }
         __syncthreads();
-        // g = Hbar[0..j+1, 0..j] * h2 (column i of Hbar has rows 0..i+1); 4 threads per row
-        const int l = t >> 2, part = t & 3;
-        for (int l0 = 0; l0 <= j + 1; l0 += TPB / 4) {
-            const int ll = l0 + l;
+        // g = Hbar[0..j+1, 0..j] * h2 (column i of Hbar has rows 0..i+1)
+        for (int l = t; l <= j + 1; l += TPB) {
             double s = 0.0;
-            if (ll <= j + 1) {
-                for (int i = (ll > 0 ? ll - 1 : 0) + part; i <= j; i += 4) {
-                    const double hv = (i == j) ? (ll == j + 1 ? sh[0] : ld(Hc, ll)) : ld(d.H, (int64_t)i * KP + ll);
-                    s += hv * (i < 1024 ? h2s[i] : ld(d.h2, i));
-                }
+            for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) {
+                const double hv = Hs ? Hs[i * J2 + l]
+                                     : (i == j ? (l == j + 1 ? sh[8] : ld(Hc, l)) : ld(d.H, (int64_t)i * KP + l));
+                s += hv * h2s[i];
             }
-            s += __shfl_xor(s, 1);
-            s += __shfl_xor(s, 2);
-            if (part == 0 && ll <= j + 1) st(d.g, ll, s);
+            st(d.g, l, s);
         }
-        if (flag) put_gram(rec, kmax, j, d.RED1 + j + 2, ld(d.RED1, j + 1), d.track_gram);
-        else if (t == 0) st(rec, rec_col(kmax), -1.0);
+        put_gram(rec, kmax, j, d.RED2 + j + 3, ld(d.RED2, j + 2), d.track_gram);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -689,11 +686,9 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
 }
 
 // ------------------------------------------------------------------ plain SpMV (test hook)
-__global__ __launch_bounds__(TPB) void k_spmv(const int* __restrict__ rowptr, const int* __restrict__ col,
-                                              const double* __restrict__ val, const double* __restrict__ x,
-                                              double* __restrict__ y, int64_t n) {
+__global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ x, double* __restrict__ y) {
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (r < n) st(y, r, spmv_row(rowptr, col, val, x, r));
+    if (r < A.n) st(y, r, spmv(A, r, [=](int64_t c) { return ld(x, c); }));
 }
 
 // ------------------------------------------------------------------ tile-major gather/scatter
@@ -734,10 +729,10 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     DISPATCH_MAXC(a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 0), s, F, a);
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(2 * a.j + 3, a.kmax, 2), s, F, a);
+    DISPATCH_MAXC(a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 2), s, F, a);
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 2, a.kmax, 1), s, F, a);
+    DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), lds_bytes(2 * a.j + 4, a.kmax, 1), s, F, a);
 }
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     DISPATCH_MAXC(a.j + 1, k_arn_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 1), s, F, a);
@@ -758,7 +753,9 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
     hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart);
 }
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
-    hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), 0, s, F, a, kind, flag, clear);
+    const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
+    const size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
+    hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), lds, s, F, a, kind, flag, clear);
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s) {
@@ -768,10 +765,9 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
     else
         hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
 }
-void launch_spmv(const int* rowptr, const int* col, const double* val, const double* x, double* y,
-                 int64_t n, hipStream_t s) {
-    const int nb = (int)((n + TPB - 1) / TPB);
-    hipLaunchKernelGGL(k_spmv, dim3(nb), dim3(TPB), 0, s, rowptr, col, val, x, y, n);
+void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
+    const int nb = (int)((A.n + TPB - 1) / TPB);
+    hipLaunchKernelGGL(k_spmv, dim3(nb), dim3(TPB), 0, s, A, x, y);
 }
 void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s) {
     const int nb = (int)((n + TPB - 1) / TPB);

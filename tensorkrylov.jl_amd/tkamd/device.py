@@ -76,6 +76,11 @@ class DeviceMatrix:
                                             L.dptr(nzval), 1 if one_based else 0, ctypes.byref(h)))
         self.h = h
 
+    @property
+    def format(self):
+        """0 = CSR, k > 0 = DIA with k diagonals."""
+        return int(self.ctx._lib.tk_matrix_format(self.h))
+
     def matvec(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
         y = np.empty(self.n)
