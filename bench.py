@@ -17,6 +17,12 @@ the scaling is STRONG (see DESIGN.md "Multi-GPU").
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
        (N > 1: launched by torch.distributed.run, one rank per GPU)
+
+Multi-rank control plane: the RCCL unique id is handed from rank 0 to the others
+through a file keyed by the launcher's pid, and the barrier / max-over-ranks use RCCL
+itself (tk_comm_allreduce_host).  torch is deliberately not imported: its wheel
+bundles its own HIP runtime, and loading it next to libtkhip would put two HIP
+runtimes in one process (DESIGN.md "Process model").
 """
 import argparse
 import json
@@ -68,20 +74,14 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
 
     d, n, cls, method, K, inst = CONFIGS[args.config]
     ctx = tkamd.Context(local_rank)
     part = tkamd.Partition(d, world, rank)
+    uid_path = None
     if world > 1:
-        import torch
-        uid = bytearray(tkamd.unique_id()) if rank == 0 else bytearray(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        ctx.init_comm(bytes(t.tolist()), world, rank)
+        uid_path = exchange_uid(tkamd, rank)
+        ctx.init_comm(uid_path[1], world, rank)
 
     csc = tkamd.assemble_matrix(n, cls)
     nnz = int(csc[0][-1])
@@ -114,8 +114,8 @@ def main():
 
     def barrier():
         ctx.sync()
-        if dist is not None:
-            dist.barrier()
+        if world > 1:
+            ctx.allreduce_host(np.zeros(1))     # RCCL all-reduce == barrier
 
     for _ in range(args.warmup):
         sweep()
@@ -129,11 +129,10 @@ def main():
     elapsed = time.perf_counter() - t0
     step_ms, step_cnt = ctx.timing_read(L.T_STEP)
     vy_ms, vy_cnt = ctx.timing_read(L.T_VY)
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
+    if world > 1:                               # max over ranks (one-hot sum)
+        v = np.zeros(world)
+        v[rank] = elapsed
+        elapsed = float(ctx.allreduce_host(v).max())
 
     # per-kernel breakdown (separate, untimed pass with per-kernel events)
     ctx.timing(2)
@@ -207,11 +206,38 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    barrier()
+    if rank == 0 and uid_path is not None:
+        try:
+            os.remove(uid_path[0])
+        except OSError:
+            pass
     dev.close()
     A.close()
     ctx.close()
-    if dist is not None:
-        dist.destroy_process_group()
+
+
+def exchange_uid(tkamd, rank, timeout=120.0):
+    """Hand the RCCL unique id from rank 0 to the other ranks of this node through a
+    file keyed by the launcher's pid (all ranks of one torch.distributed.run share it)."""
+    key = "%d_%s" % (os.getppid(), os.environ.get("MASTER_PORT", "0"))
+    path = os.path.join("/tmp", "tkhip_uid_%s.bin" % key)
+    if rank == 0:
+        uid = tkamd.unique_id()
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return path, uid
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > timeout:
+            raise RuntimeError("rank %d: no RCCL unique id from rank 0 after %.0f s" % (rank, timeout))
+        time.sleep(0.01)
+    with open(path, "rb") as f:
+        uid = f.read()
+    assert len(uid) == 128
+    return path, uid
 
 
 def cpu_baseline(csc, n, d, K, seconds):

@@ -1,0 +1,43 @@
+"""gloo worker for tests/test_dist_cpu.py -- TEST INFRASTRUCTURE ONLY.
+
+Runs the product's tensorkrylov host loop on this rank's block of factors (CPU
+stand-in device, tests/_fake_device.py) with the per-step records summed over ranks
+by torch.distributed (gloo), and writes rank-local results as JSON."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "tensorkrylov.jl_amd"), os.path.dirname(HERE)]
+
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import tkamd  # noqa: E402
+from _fake_device import backend  # noqa: E402
+
+
+def main():
+    out, method, d, K = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = 200
+    rng = np.random.default_rng(777)
+    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    A = tkamd.KroneckerMatrix.gallery(tkamd.SymInstance, d, n, tkamd.Laplace)
+    conv = tkamd.ConvergenceData(K)
+    part = tkamd.Partition(d, world, rank)
+    x = tkamd.tensorkrylov(conv, A, b, 1e-9, K, method, partition=part, backend=backend)
+    res = {"rank": rank, "world": world, "local": list(part.local()),
+           "relres": conv.relative_residual_norm.tolist(), "proj": conv.projected_residual_norm.tolist(),
+           "orth": conv.orthogonality_data.tolist(), "niter": conv.niterations,
+           "x_factors": None if x is None else x.factors}
+    with open("%s.%d.json" % (out, rank), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

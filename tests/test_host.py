@@ -1,0 +1,225 @@
+"""CPU tests of the product's host side (no GPU): gallery, compressed-side numerics,
+record bookkeeping, partitioning, the C-ABI library's exports, and the whole
+tensorkrylov driver loop over a CPU stand-in device (tests/_fake_device.py)."""
+import math
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import tkamd
+from oracle import tk_oracle as O
+from tkamd import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+# ------------------------------------------------------------------ gallery
+@pytest.mark.parametrize("n", [1, 2, 3, 200, 257, 1000])
+@pytest.mark.parametrize("cls", ["Laplace", "ConvDiff"])
+def test_gallery_bit_identical_to_reference_assembly(n, cls):
+    a = tkamd.assemble_matrix(n, cls)
+    A = O.laplace_dense(n) if cls == "Laplace" else O.convdiff_dense(n)
+    o = O.dense_to_csc(A)
+    for x, y in zip(a, o):
+        assert np.array_equal(x, y)
+
+
+def test_rand_sparse_spd_generator():
+    colptr, rowval, nz = tkamd.assemble_matrix(4000, "RandSparseSPD")
+    n = 4000
+    A = np.zeros((n, n))
+    for j in range(n):
+        A[rowval[colptr[j]:colptr[j + 1]], j] = nz[colptr[j]:colptr[j + 1]]
+    assert np.array_equal(A, A.T)
+    off = np.abs(A).sum(axis=1) - np.abs(np.diag(A))
+    assert np.all(np.diag(A) > off)                     # strictly diagonally dominant -> SPD
+    assert 20 <= len(nz) / n <= 30                      # ~14 draws + transpose + diagonal
+    assert np.all(np.diff(colptr) > 0)
+    # rows sorted within columns (CSC invariant)
+    for j in range(0, n, 97):
+        assert np.all(np.diff(rowval[colptr[j]:colptr[j + 1]]) > 0)
+
+
+# ------------------------------------------------------------------ compressed side
+@pytest.mark.parametrize("d,k,t", [(2, 4, 3), (3, 5, 4), (5, 7, 6), (4, 6, 1), (6, 3, 5)])
+def test_residual_vectorized_matches_reference_loops(d, k, t):
+    rng = np.random.default_rng(100 * d + k)
+    Hs = [rng.standard_normal((k, k)) for _ in range(d)]
+    Ys = [0.3 * rng.standard_normal((k, t)) for _ in range(d)]
+    lam = rng.random(t)
+    sub = list(rng.random(d))
+    bt = [rng.standard_normal(k) for _ in range(d)]
+    try:
+        ro = O.residualnorm(Hs, lam, Ys, k, sub, bt, 1.3)
+    except O.CompressedNormBreakdown:
+        ro = None
+    try:
+        rp = tkamd.residualnorm(Hs, lam, Ys, k, sub, bt, 1.3)
+    except tkamd.CompressedNormBreakdown:
+        rp = None
+    if ro is None:
+        assert rp is None
+    else:
+        assert math.isclose(ro[0], rp[0], rel_tol=1e-12, abs_tol=1e-14)
+        assert math.isclose(ro[1], rp[1], rel_tol=1e-12)
+
+
+def test_compressed_breakdown_raised():
+    # a residual whose compressed part is negative must raise (src/utils.jl:395)
+    k, t = 3, 2
+    Hs = [np.zeros((k, k))]
+    Ys = [np.zeros((k, t))]
+    bt = [np.zeros(k)]
+    Ys[0][0, :] = 1.0
+    Hs[0][:] = np.eye(k)
+    with pytest.raises(tkamd.CompressedNormBreakdown):
+        # Hy_norm = 0 here is impossible; use b_norm large so -2<Hy,b> dominates
+        tkamd.residualnorm(Hs, np.array([1.0, 1.0]), Ys, k, [0.0], bt, 10.0)
+
+
+@pytest.mark.parametrize("sym", [True, False])
+def test_compressed_solve_matches_reference(sym):
+    rng = np.random.default_rng(5)
+    k = 9
+    H = O.laplace_dense(20)[:k, :k] if sym else O.convdiff_dense(20)[:k, :k]
+    bt = [rng.random(k) for _ in range(3)]
+    if sym:
+        rank, al, om = O.sym_expsum(O.ExpSumTables(), 437.0, 1e-9)
+    else:
+        rank, al, om = O.nonsym_expsum(3000.0, 1e-9)
+    ap = tkamd.ApproximationData(1e-9, sym)
+    ap.alpha, ap.omega = al, om
+    l1, Y1 = O.solve_compressed_system(H, bt, al, om, 7.5, sym)
+    l2, Y2 = tkamd.solve_compressed_system(H, bt, ap, 7.5, sym)
+    assert np.allclose(l1, l2, rtol=1e-15, atol=0)
+    scale = max(np.abs(y).max() for y in Y1)
+    assert max(np.abs(a - b).max() for a, b in zip(Y1, Y2)) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("kappa", [1.5, 2.0, 9.99, 10.0, 123.4, 999.0, 1054.2, 16534.0, 3.3e7])
+@pytest.mark.parametrize("tol", [1e-9, 1e-6, 1e-12])
+def test_expsum_rank_and_coefficients(kappa, tol):
+    class S:
+        def current(self):
+            return 1.0, kappa, kappa
+    ap = tkamd.ApproximationData(tol, True)
+    try:
+        rank, al, om = O.sym_expsum(O.ExpSumTables(), kappa, tol)
+    except ValueError:
+        with pytest.raises(ValueError):
+            ap.update(S())
+        return
+    ap.update(S())
+    assert ap.rank == rank
+    assert np.array_equal(ap.alpha, al) and np.array_equal(ap.omega, om)
+
+
+@pytest.mark.parametrize("lmin", [1.0, 37.0, 4e4, 2e5])
+def test_nonsym_expsum(lmin):
+    class S:
+        def current(self):
+            return lmin, math.inf, math.inf
+    ap = tkamd.ApproximationData(1e-9, False)
+    ap.update(S())
+    rank, al, om = O.nonsym_expsum(lmin, 1e-9)
+    assert ap.rank == rank and len(ap.alpha) == 2 * rank + 1
+    assert np.allclose(ap.alpha, al, rtol=1e-15) and np.allclose(ap.omega, om, rtol=1e-15)
+
+
+def test_spectral_data_laplace_and_convdiff():
+    for cls, inst in (("Laplace", tkamd.SymInstance), ("ConvDiff", tkamd.NonSymInstance)):
+        d, n = 4, 120
+        A = tkamd.KroneckerMatrix.gallery(inst, d, n, cls)
+        sp = tkamd.SpectralData(A, 30)
+        dense = O.laplace_dense(n) if cls == "Laplace" else O.convdiff_dense(n)
+        for k in range(2, 30):
+            sp.update(d)
+            ref = O.spectral_update(cls, inst == tkamd.SymInstance, d, n, k, dense[:k, :k])
+            assert math.isclose(sp.lmin[k - 1], ref[0], rel_tol=1e-12)
+            if inst == tkamd.SymInstance:
+                assert math.isclose(sp.kappa[k - 1], ref[2], rel_tol=1e-12)
+
+
+# ------------------------------------------------------------------ partition / records
+@pytest.mark.parametrize("d,N", [(8, 1), (8, 2), (8, 8), (10, 8), (5, 8), (4, 3)])
+def test_partition(d, N):
+    parts = [tkamd.Partition(d, N, r) for r in range(N)]
+    owned = [s for p in parts for s in p.local()]
+    assert owned == list(range(d))
+    assert max(p.nf for p in parts) - min(p.nf for p in parts) <= 1
+
+
+def test_reorth_record_bookkeeping():
+    """LanczosReorth H mirror: MGS column, H[1:k-2,k] = 0, update_subdiagonals!."""
+    K = 6
+    td = tkamd.TensorLanczosReorth(tkamd.KroneckerMatrix(tkamd.SymInstance, [tkamd.assemble_matrix(10, 'Laplace')]), K)
+    lay = td.layout
+    rec = np.zeros((1, lay.m))
+    j = 4
+    rec[0, :j + 2] = np.arange(1, j + 3, dtype=float)   # MGS column 1..6
+    rec[0, lay.flag] = 1.0
+    rec[0, lay.loss] = 1e-7
+    td._apply_step(j, rec)
+    col = td.H[0, :, j]
+    assert np.all(col[:j - 1] == 0.0)                   # rows 0..j-2 zeroed
+    assert col[j - 1] == j and col[j] == j + 1          # MGS values kept
+    assert col[j + 1] == j + 2 and td.H[0, j, j + 1] == j + 2
+
+
+# ------------------------------------------------------------------ C ABI library
+def _header_symbols():
+    hdr = open(os.path.join(ROOT, "include", "tk.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    return set(re.findall(r"\b(tk_[a-z_0-9]+)\s*\(", hdr))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = os.path.join(ROOT, "tensorkrylov.jl_amd", "tkamd", "libtkhip.so")
+    assert os.path.exists(lib), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (tk_[a-z_0-9]+)$", out, flags=re.M))
+    declared = _header_symbols()
+    assert declared == set(L.EXPORTS)
+    assert declared <= exported, declared - exported
+    # C linkage only: no mangled tk entry points leak from the ABI
+    assert not [s for s in exported if s.startswith("_Z")]
+
+
+def test_library_loads_and_fails_loudly_without_gpu():
+    lib = L.lib()
+    assert lib.tk_version() == 100
+    assert lib.tk_record_len(50) == 110
+    # (torch is deliberately not imported here: it bundles its own HIP runtime, and
+    # loading it after libtkhip would put two runtimes in one process -- DESIGN.md)
+    try:
+        tkamd.Context(0).close()
+    except tkamd.TKError as e:
+        assert "no HIP device" in str(e) or "gfx950" in str(e)
+    # null handles are rejected with a status, never a crash
+    assert lib.tk_decomp_step(None, 0, None) != 0
+    assert b"NULL" in lib.tk_last_error()
+
+
+# ------------------------------------------------------------------ whole driver, CPU device stand-in
+@pytest.mark.parametrize("method,cls,sym,d,K", [("TensorArnoldi", "Laplace", True, 3, 30),
+                                                  ("TensorLanczosReorth", "Laplace", True, 3, 30),
+                                                  ("TensorLanczos", "Laplace", True, 2, 20),
+                                                  ("TensorArnoldi", "ConvDiff", False, 3, 15)])
+def test_driver_host_logic_matches_oracle(method, cls, sym, d, K):
+    from _fake_device import backend
+    n = 200
+    rng = np.random.default_rng(12345)
+    b = tkamd.normalize_rhs(tkamd.random_rhs(d, n, rng))
+    inst = tkamd.SymInstance if sym else tkamd.NonSymInstance
+    A = tkamd.KroneckerMatrix.gallery(inst, d, n, cls)
+    conv = tkamd.ConvergenceData(K)
+    tkamd.tensorkrylov(conv, A, b, 1e-9, K, method, backend=backend)
+    dense = O.laplace_dense(n) if cls == "Laplace" else O.convdiff_dense(n)
+    conv_o, _, _ = O.tensorkrylov([O.dense_to_csc(dense)] * d, b, 1e-9, K, method, cls, sym, A_dense=dense)
+    assert conv.niterations == conv_o.niterations
+    ref = np.array(conv_o.relative_residual_norm)
+    assert np.abs(conv.relative_residual_norm - ref).max() <= 1e-12 * ref.max()
+    assert np.allclose(conv.orthogonality_data[1:], conv_o.orthogonality_data[1:], rtol=1e-6, atol=1e-15)
