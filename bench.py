@@ -63,6 +63,8 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--pmc-mode", action="store_true",
+                    help="run exactly one untimed sweep (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
 
     import tkamd
@@ -116,6 +118,14 @@ def main():
         ctx.sync()
         if world > 1:
             ctx.allreduce_host(np.zeros(1))     # RCCL all-reduce == barrier
+
+    if args.pmc_mode:
+        sweep()
+        barrier()
+        dev.close()
+        A.close()
+        ctx.close()
+        return
 
     for _ in range(args.warmup):
         sweep()

@@ -89,9 +89,10 @@ tk_status tk_matrix_from_csr(tk_ctx* ctx, int64_t n, const int64_t* rowptr,
                              const int64_t* colind, const double* val,
                              int one_based, tk_mat** out);
 tk_status tk_matrix_destroy(tk_mat* A);
-/* Storage chosen on the device: 0 = CSR, k > 0 = DIA with k diagonals (banded
- * matrices with few, mostly full diagonals; no index loads in the SpMV).  Both keep
- * the per-row ascending-column summation order.  TKHIP_FORCE_CSR=1 forces CSR. */
+/* Storage chosen on the device: k > 0 = DIA with k diagonals (banded matrices with
+ * few, mostly full diagonals; no index loads), -2 = SELL-256 (sliced ELL, one slice
+ * per 256-row tile: coalesced index/value loads), 0 = CSR.  All keep the per-row
+ * ascending-column summation order.  TKHIP_FORCE_CSR=1 forces CSR. */
 int tk_matrix_format(tk_mat* A);
 /* y = A x on the device (host in/out buffers; test hook for mul!, used at
  * src/orthogonal_bases.jl:20,45,103). */

@@ -57,7 +57,8 @@ enum { TCLS_STEP = 0, TCLS_PASS1 = 1, TCLS_PASS2 = 2, TCLS_FIN = 3, TCLS_RED = 4
 
 struct tk_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;    // compute
+    hipStream_t xstream = nullptr;   // per-step record exchange (RCCL), overlaps compute
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     int timing = 0;   // 0 off, 1 step level, 2 per kernel class
@@ -72,17 +73,19 @@ struct Timer {
     tk_ctx* c;
     int cls;
     bool on;
+    hipStream_t st;
     hipEvent_t b = nullptr;
-    Timer(tk_ctx* c_, int cls_, int level) : c(c_), cls(cls_), on(c_->timing >= level) {
+    Timer(tk_ctx* c_, int cls_, int level, hipStream_t s_ = nullptr)
+        : c(c_), cls(cls_), on(c_->timing >= level), st(s_ ? s_ : c_->stream) {
         if (!on) return;
         hipEvent_t a;
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
-        hipEventRecord(a, c->stream);
+        hipEventRecord(a, st);
         c->ev[cls].push_back(a);
     }
     ~Timer() {
         if (!on) return;
-        hipEventRecord(b, c->stream);
+        hipEventRecord(b, st);
         c->ev[cls].push_back(b);
     }
 };
@@ -123,6 +126,7 @@ tk_status tk_ctx_create(int device, tk_ctx** out) {
     tk_ctx* c = new tk_ctx();
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return fail(TK_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -135,10 +139,12 @@ tk_status tk_ctx_destroy(tk_ctx* c) {
     if (!c) return TK_OK;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(c->xstream);
     drain_timers(c);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->xbuf) hipFree(c->xbuf);
     hipStreamDestroy(c->stream);
+    hipStreamDestroy(c->xstream);
     delete c;
     return TK_OK;
 }
@@ -147,6 +153,7 @@ tk_status tk_ctx_sync(tk_ctx* c) {
     CHECKARG(c, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->xstream));
     return TK_OK;
 }
 
@@ -181,6 +188,7 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) {
         HIPCHK(hipMalloc(&c->xbuf, count * sizeof(double)));
         c->xcap = count;
     }
+    HIPCHK(hipStreamSynchronize(c->xstream));
     HIPCHK(hipMemcpyAsync(c->xbuf, buf, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclAllReduce(c->xbuf, c->xbuf, count, ncclDouble, ncclSum, c->comm, c->stream));
     HIPCHK(hipMemcpyAsync(buf, c->xbuf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -199,6 +207,12 @@ struct tk_mat {
     double* dval = nullptr;
     int ndiag = 0;
     int64_t dld = 0;
+    long long* sptr = nullptr;
+    int* swidth = nullptr;
+    int* rowlen = nullptr;
+    int* scol = nullptr;
+    double* sval = nullptr;
+    int sell = 0;
     SpM spm() const {
         SpM m;
         m.rowptr = rowptr;
@@ -208,6 +222,12 @@ struct tk_mat {
         m.dval = dval;
         m.ndiag = ndiag;
         m.dld = dld;
+        m.sptr = sptr;
+        m.swidth = swidth;
+        m.rowlen = rowlen;
+        m.scol = scol;
+        m.sval = sval;
+        m.sell = sell;
         m.n = n;
         return m;
     }
@@ -219,6 +239,11 @@ static void free_mat(tk_mat* A) {
     hipFree(A->val);
     hipFree(A->doff);
     hipFree(A->dval);
+    hipFree(A->sptr);
+    hipFree(A->swidth);
+    hipFree(A->rowlen);
+    hipFree(A->scol);
+    hipFree(A->sval);
     delete A;
 }
 
@@ -254,6 +279,47 @@ static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<i
     offs = seen;
 }
 
+// SELL-256 (sliced ELL, slice = 256-row tile) for matrices that are not banded, when the
+// padding stays within 2x nnz; TKHIP_FORCE_CSR=1 disables it.
+static bool build_sell(int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
+                       const std::vector<double>& v, std::vector<long long>& sptr, std::vector<int>& sw,
+                       std::vector<int>& rl, std::vector<int>& sc, std::vector<double>& sv) {
+    const char* env = getenv("TKHIP_FORCE_CSR");
+    if (env && env[0] == '1') return false;
+    const int64_t nt = (n + 255) / 256;
+    sptr.assign(nt, 0);
+    sw.assign(nt, 0);
+    rl.assign(nt * 256, 0);
+    long long slots = 0;
+    for (int64_t t = 0; t < nt; ++t) {
+        int w = 0;
+        for (int64_t r = t * 256; r < std::min<int64_t>(n, (t + 1) * 256); ++r) {
+            rl[r] = rp[r + 1] - rp[r];
+            w = std::max(w, rl[r]);
+        }
+        sptr[t] = slots;
+        sw[t] = w;
+        slots += (long long)w * 256;
+    }
+    if (slots > 2 * (long long)ci.size() + 256 || slots >= (long long)INT32_MAX) return false;
+    sc.assign(slots, 0);
+    sv.assign(slots, 0.0);
+    for (int64_t t = 0; t < nt; ++t)
+        for (int l = 0; l < 256; ++l) {
+            const int64_t r = t * 256 + l;
+            for (int q = 0; q < sw[t]; ++q) {
+                const long long e = sptr[t] + (long long)q * 256 + l;
+                if (r < n && q < rl[r]) {
+                    sc[e] = ci[rp[r] + q];
+                    sv[e] = v[rp[r] + q];
+                } else {
+                    sc[e] = (int)std::min<int64_t>(r, n - 1);
+                }
+            }
+        }
+    return true;
+}
+
 static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
                             const std::vector<double>& v, tk_mat** out) {
     tk_mat* A = new tk_mat();
@@ -276,6 +342,24 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
         if (e == hipSuccess) e = hipMalloc(&A->dval, dv.size() * sizeof(double));
         if (e == hipSuccess) e = hipMemcpy(A->doff, offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(A->dval, dv.data(), dv.size() * sizeof(double), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess && offs.empty()) {
+        std::vector<long long> sptr;
+        std::vector<int> sw, rl, sc;
+        std::vector<double> sv;
+        if (build_sell(n, rp, ci, v, sptr, sw, rl, sc, sv)) {
+            A->sell = 1;
+            e = hipMalloc(&A->sptr, sptr.size() * sizeof(long long));
+            if (e == hipSuccess) e = hipMalloc(&A->swidth, sw.size() * sizeof(int));
+            if (e == hipSuccess) e = hipMalloc(&A->rowlen, rl.size() * sizeof(int));
+            if (e == hipSuccess) e = hipMalloc(&A->scol, std::max<size_t>(sc.size(), 1) * sizeof(int));
+            if (e == hipSuccess) e = hipMalloc(&A->sval, std::max<size_t>(sv.size(), 1) * sizeof(double));
+            if (e == hipSuccess) e = hipMemcpy(A->sptr, sptr.data(), sptr.size() * sizeof(long long), hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(A->swidth, sw.data(), sw.size() * sizeof(int), hipMemcpyHostToDevice);
+            if (e == hipSuccess) e = hipMemcpy(A->rowlen, rl.data(), rl.size() * sizeof(int), hipMemcpyHostToDevice);
+            if (e == hipSuccess && !sc.empty()) e = hipMemcpy(A->scol, sc.data(), sc.size() * sizeof(int), hipMemcpyHostToDevice);
+            if (e == hipSuccess && !sv.empty()) e = hipMemcpy(A->sval, sv.data(), sv.size() * sizeof(double), hipMemcpyHostToDevice);
+        }
     }
     if (e != hipSuccess) {
         free_mat(A);
@@ -346,7 +430,7 @@ tk_status tk_matrix_destroy(tk_mat* A) {
     return TK_OK;
 }
 
-int tk_matrix_format(tk_mat* A) { return A ? A->ndiag : -1; }
+int tk_matrix_format(tk_mat* A) { return A ? (A->ndiag > 0 ? A->ndiag : (A->sell ? -2 : 0)) : -1; }
 
 tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
     CHECKARG(A && x && y, "NULL argument");
@@ -375,6 +459,7 @@ struct tk_decomp {
     int64_t n, ld;
     int ntiles, npart;
     int jnext = 0;          // next step index
+    int fmt = 0;            // SpMV storage shared by all local factors (KArgs::fmt)
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
     int last_j = -1;
@@ -390,6 +475,9 @@ struct tk_decomp {
     double* scratch = nullptr;   // column gather buffer (n x 8)
     // host Gram mirror (LanczosReorth decisions): [nf][(kmax+1)^2]
     std::vector<std::vector<double>> gram;
+    // per-slot events: compute -> exchange (slot written) and exchange -> compute
+    // (the all-reduce has finished reading the slot's send rows)
+    std::vector<hipEvent_t> ev_c, ev_x;
 };
 
 int tk_record_len(int kmax) { return rec_len(kmax); }
@@ -404,6 +492,8 @@ static tk_status dalloc(tk_decomp* dc, void** p, size_t bytes) {
 }
 
 static void free_decomp(tk_decomp* dc) {
+    for (hipEvent_t e : dc->ev_c) hipEventDestroy(e);
+    for (hipEvent_t e : dc->ev_x) hipEventDestroy(e);
     for (void* p : dc->allocs) hipFree(p);
     if (dc->scratch) hipFree(dc->scratch);
     if (dc->Ydev) hipFree(dc->Ydev);
@@ -472,6 +562,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
     }
+    {
+        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? 1 : (A->sell ? 2 : 3); };
+        dc->fmt = fmt_of(mats[0]);
+        for (int f = 1; f < nf; ++f)
+            if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;
+    }
     DA(dc->df, nf * sizeof(DFac));
     DA(dc->dsub, nf * sizeof(DFac));
     {
@@ -485,6 +581,18 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->recv = dc->rec;
 #undef DA
     if (method == TK_LANCZOS_REORTH) dc->gram.assign(nf, std::vector<double>((size_t)KC * KC, 0.0));
+    if (dc->recv != dc->rec) {
+        dc->ev_c.assign(kmax + 2, nullptr);
+        dc->ev_x.assign(kmax + 2, nullptr);
+        for (int i = 0; i < kmax + 2; ++i) {
+            hipError_t e = hipEventCreateWithFlags(&dc->ev_c[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&dc->ev_x[i], hipEventDisableTiming);
+            if (e != hipSuccess) {
+                free_decomp(dc);
+                return fail(TK_ERR_HIP, "hipEventCreate: %s", hipGetErrorString(e));
+            }
+        }
+    }
     *out = dc;
     return TK_OK;
 }
@@ -494,6 +602,13 @@ tk_status tk_decomp_destroy(tk_decomp* dc) {
     hipSetDevice(dc->ctx->device);
     hipStreamSynchronize(dc->ctx->stream);
     free_decomp(dc);
+    return TK_OK;
+}
+
+// Before a slot's send rows are rewritten, the previous all-reduce of that slot must
+// have finished reading them.
+static tk_status slot_guard(tk_decomp* dc, int slot) {
+    if (dc->recv != dc->rec) HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[slot], 0));
     return TK_OK;
 }
 
@@ -507,6 +622,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.kmax = dc->kmax;
     a.m = dc->m;
     a.rec = dc->rec + (size_t)slot * dc->d_total * dc->m;
+    a.fmt = dc->fmt;
     return a;
 }
 
@@ -519,8 +635,19 @@ static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out) {
     double* s = dc->rec + (size_t)slot * cnt;
     double* r = dc->recv + (size_t)slot * cnt;
     if (dc->recv != dc->rec) {
-        Timer tm(c, TCLS_XCH, 2);
-        NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->stream));
+        // the exchange runs on its own stream, overlapping the next step's kernels
+        HIPCHK(hipEventRecord(dc->ev_c[slot], c->stream));
+        HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[slot], 0));
+        {
+            Timer tm(c, TCLS_XCH, 2, c->xstream);
+            NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->xstream));
+        }
+        HIPCHK(hipEventRecord(dc->ev_x[slot], c->xstream));
+        if (rec_out) {
+            HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->xstream));
+            HIPCHK(hipStreamSynchronize(c->xstream));
+        }
+        return TK_OK;
     }
     if (rec_out) {
         HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -547,7 +674,8 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    tk_status st = TK_OK;
+    tk_status st = slot_guard(dc, 0);
+    if (st) return st;
     KArgs a = base_args(dc, 0, 0);
     const int nf = dc->nf;
     RUN(TCLS_PASS1, 2, launch_init_a(dc->df, nf, a, s), "init_a");
@@ -605,6 +733,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_ctx* c = dc->ctx;
     hipStream_t s = c->stream;
     const int nf = dc->nf, slot = j + 1;
+    tk_status st = slot_guard(dc, slot);
+    if (st) return st;
     KArgs a = base_args(dc, j, slot);
     Timer step_timer(c, TCLS_STEP, 1);
     if (dc->method == TK_ARNOLDI) {
@@ -735,8 +865,10 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {
         }
         return TK_OK;
     }
+    tk_status st = slot_guard(dc, slot);
+    if (st) return st;
     KArgs a = base_args(dc, dc->last_j, slot);
-    tk_status st = finalize_pending(dc, a);
+    st = finalize_pending(dc, a);
     if (st) return st;
     dc->pending = false;
     return exchange_and_copy(dc, slot, rec_out);
@@ -747,6 +879,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
     CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
     HIPCHK(hipSetDevice(dc->ctx->device));
     const size_t per = (size_t)dc->d_total * dc->m;
+    HIPCHK(hipStreamSynchronize(dc->ctx->xstream));
     HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                           dc->ctx->stream));
     HIPCHK(hipStreamSynchronize(dc->ctx->stream));

@@ -26,8 +26,15 @@ struct SpM {
     const double* val;    // (nnz)
     const int* doff;      // DIA offsets (ndiag), ascending
     const double* dval;   // DIA values [ndiag][dld]: dval[q*dld + r] = A[r, r + doff[q]]
-    int ndiag;            // 0 = CSR only
+    int ndiag;            // > 0: DIA is used
     int64_t dld;
+    // SELL-256: slice = one 256-row tile; entry q of row r at sptr[r/256] + q*256 + r%256
+    const long long* sptr;  // (ntiles) slot offset of each slice
+    const int* swidth;    // (ntiles) slice width = max row length in the slice
+    const int* rowlen;    // (ntiles*256) row lengths (0 for padding rows)
+    const int* scol;      // (slots) column, padded entries repeat the row index
+    const double* sval;   // (slots) value, padded entries 0
+    int sell;             // 1: SELL is used (when ndiag == 0)
     int64_t n;
 };
 
@@ -60,6 +67,7 @@ struct KArgs {
     int kmax;
     int m;            // record length per factor
     double* rec;      // record slot base ([d_total][m])
+    int fmt;          // storage common to all factors of the launch: 1 DIA, 2 SELL, 3 CSR, 0 mixed
 };
 
 // launchers (tk_kernels.hip)

@@ -190,15 +190,28 @@ __device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, 
 
 // y[r] = sum over row r of A, terms in ascending column order, products and sums
 // separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
-template <class XF>
+// FMT: SPM_DIA / SPM_SELL / SPM_CSR fixes the storage at compile time (fewer live
+// registers in the fused kernels); SPM_ANY decides at run time.
+enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3 };
+template <int FMT, class XF>
 __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
 #pragma clang fp contract(off)
     double s = 0.0;
-    if (A.ndiag > 0) {
+    if (FMT == SPM_DIA || (FMT == SPM_ANY && A.ndiag > 0)) {
         for (int q = 0; q < A.ndiag; ++q) {
             const int64_t c = r + GP(const int, A.doff)[q];
             const double v = ld(A.dval, (int64_t)q * A.dld + r);
             if (c >= 0 && c < A.n) s = add_rn(s, mul_rn(v, x(c)));
+        }
+    } else if (FMT == SPM_SELL || (FMT == SPM_ANY && A.sell)) {
+        const int64_t t = r >> 8;
+        const int l = (int)(r & 255);
+        const int64_t base = GP(const long long, A.sptr)[t];
+        const int w = GP(const int, A.swidth)[t];
+        const int len = GP(const int, A.rowlen)[r];
+        for (int q = 0; q < w; ++q) {
+            const int64_t e = base + (int64_t)q * TPB + l;
+            if (q < len) s = add_rn(s, mul_rn(ld(A.sval, e), x((int64_t)GP(const int, A.scol)[e])));
         }
     } else {
         const int p0 = GP(const int, A.rowptr)[r], p1 = GP(const int, A.rowptr)[r + 1];
@@ -259,7 +272,7 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 // ------------------------------------------------------------------ Arnoldi (CGS2)
 
 // First pass, v_j stored:  W = A v_j;  P1 = [ <V[:,c], W>, c = 0..j ].
-template <int MAXC>
+template <int MAXC, int FMT>
 __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     double* acc = lds;
@@ -269,7 +282,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
         Row<MAXC> R;
         R.load(tv, toff);
         const double* Vg = d.V;
-        const double w = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
+        const double w = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, nc, w, tr, acc, 0, first);
     }
@@ -280,7 +293,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
 //   v_j = (U - V[:,0..j) h2) * inv_beta                     -> V[:, j]
 //   W   = (A U - V[:,0..j) g[0..j) - g[j] v_j) * inv_beta    (= A v_j, Arnoldi relation)
 //   P1  = [ <V[:,c],W> (c<j), <v_j,W> ]
-template <int MAXC>
+template <int MAXC, int FMT>
 __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j;
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F
         Row<MAXC> R;
         R.load(tv, toff);
         const double* Ug = d.U;
-        const double au = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
+        const double au = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double w = ok ? (au - row_dot(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
@@ -370,6 +383,7 @@ __global__ __launch_bounds__(TPB) void k_arn_finalize(const DFac* __restrict__ F
 
 // Plain, v_j stored (src/orthogonal_bases.jl:45-50):
 //   U = A v_j - beta_{j-1} v_{j-1};  P1 = [ <U, v_j> ]
+template <int FMT>
 __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
@@ -378,7 +392,7 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F
     const double bp = j > 0 ? ld(d.sc, SC_BETAPREV) : 0.0;
     TILE_LOOP
         const double* Vg = d.V;
-        const double av = ok ? spmv(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
+        const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
         const double prev = j > 0 ? ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x) : 0.0;
         const double u = av - bp * prev;
         const double v = ld(Vt, (int64_t)j * TPB + threadIdx.x);
@@ -392,6 +406,7 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F
 // Fused: pending v_j = (beta == 0 ? 0 : inv(beta) .* W) (src/orthogonal_bases.jl:59) is
 // written while  U = A v_j - beta v_{j-1};
 //   P1 = [ <U,v_j>, <v_j,b> | gram <V[:,c],v_j> (c<j), <v_j,v_j> ]
+template <int FMT>
 __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     KERNEL_PROLOGUE
@@ -404,7 +419,7 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F
     TILE_LOOP
         const double vj = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
         const double* Wg = d.W;
-        const double av = ok ? spmv(d.A, r, [=](int64_t c) { return zero ? 0.0 : mul_rn(ld(Wg, c), inv_beta); }) : 0.0;
+        const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return zero ? 0.0 : mul_rn(ld(Wg, c), inv_beta); }) : 0.0;
         const double u = av - beta * ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x);
         st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
         st(d.U, r, u);
@@ -688,7 +703,7 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
 // ------------------------------------------------------------------ plain SpMV (test hook)
 __global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ x, double* __restrict__ y) {
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (r < A.n) st(y, r, spmv(A, r, [=](int64_t c) { return ld(x, c); }));
+    if (r < A.n) st(y, r, spmv<SPM_ANY>(A, r, [=](int64_t c) { return ld(x, c); }));
 }
 
 // ------------------------------------------------------------------ tile-major gather/scatter
@@ -725,11 +740,41 @@ void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_init_b, dim3(a.npart, nf), dim3(TPB), lds_bytes(2, a.kmax, 0), s, F, a);
 }
+#define DISPATCH_FMT_MAXC(fmt, ncols, KERNEL, ...)                                  \
+    do {                                                                            \
+        switch (fmt) {                                                              \
+            case SPM_DIA: DISPATCH_MAXC2(ncols, KERNEL, SPM_DIA, __VA_ARGS__); break;   \
+            case SPM_SELL: DISPATCH_MAXC2(ncols, KERNEL, SPM_SELL, __VA_ARGS__); break; \
+            case SPM_CSR: DISPATCH_MAXC2(ncols, KERNEL, SPM_CSR, __VA_ARGS__); break;   \
+            default: DISPATCH_MAXC2(ncols, KERNEL, SPM_ANY, __VA_ARGS__); break;        \
+        }                                                                           \
+    } while (0)
+#define DISPATCH_MAXC2(ncols, KERNEL, F_, ...)                   \
+    do {                                                         \
+        if ((ncols) <= 16)                                       \
+            hipLaunchKernelGGL((KERNEL<16, F_>), __VA_ARGS__);   \
+        else if ((ncols) <= 32)                                  \
+            hipLaunchKernelGGL((KERNEL<32, F_>), __VA_ARGS__);   \
+        else if ((ncols) <= 48)                                  \
+            hipLaunchKernelGGL((KERNEL<48, F_>), __VA_ARGS__);   \
+        else                                                     \
+            hipLaunchKernelGGL((KERNEL<64, F_>), __VA_ARGS__);   \
+    } while (0)
+#define DISPATCH_FMT(fmt, KERNEL, ...)                                                          \
+    do {                                                                                        \
+        switch (fmt) {                                                                          \
+            case SPM_DIA: hipLaunchKernelGGL((KERNEL<SPM_DIA>), __VA_ARGS__); break;            \
+            case SPM_SELL: hipLaunchKernelGGL((KERNEL<SPM_SELL>), __VA_ARGS__); break;          \
+            case SPM_CSR: hipLaunchKernelGGL((KERNEL<SPM_CSR>), __VA_ARGS__); break;            \
+            default: hipLaunchKernelGGL((KERNEL<SPM_ANY>), __VA_ARGS__); break;                 \
+        }                                                                                       \
+    } while (0)
+
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 0), s, F, a);
+    DISPATCH_FMT_MAXC(a.fmt, a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 0), s, F, a);
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 2), s, F, a);
+    DISPATCH_FMT_MAXC(a.fmt, a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 2), s, F, a);
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), lds_bytes(2 * a.j + 4, a.kmax, 1), s, F, a);
@@ -738,10 +783,10 @@ void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     DISPATCH_MAXC(a.j + 1, k_arn_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 1), s, F, a);
 }
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_l1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
+    DISPATCH_FMT(a.fmt, k_lan_l1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_lan_l1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
+    DISPATCH_FMT(a.fmt, k_lan_l1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);

@@ -50,6 +50,8 @@ def test_spmv_bit_exact(ctx, cls, n, force_csr, monkeypatch):
     A = tk.DeviceMatrix(ctx, csc)
     expect_dia = (not force_csr) and cls in ("Laplace", "ConvDiff")
     assert (A.format > 0) == expect_dia
+    if not force_csr and cls == "RandSparseSPD":
+        assert A.format == -2                       # SELL-256
     x = np.random.default_rng(1).standard_normal(n)
     y = A.matvec(x)
     y_ref = O.csc_matvec_fast(csc, x)
@@ -147,7 +149,7 @@ def test_lanczos_reorth_matches_oracle(ctx):
     the test therefore (1) checks each device decision against the device's own loss,
     (2) checks that loss against the loss of the device's V computed here, (3) drives
     the oracle with the device's decisions and compares H and V, and (4) requires the
-    free-running oracle to agree wherever its loss is not within 2x of sqrt(eps)."""
+    free-running oracle to agree wherever its loss is not within 10x of sqrt(eps)."""
     import math
     tk = _tk()
     n, K = 300, 60
@@ -174,13 +176,14 @@ def test_lanczos_reorth_matches_oracle(ctx):
         td._apply_step(j, recs[j + 1])
     scale = np.abs(fo.H[:K + 1, :K]).max()
     assert np.abs(td.H[0, :K + 1, :K] - fo.H[:K + 1, :K]).max() <= 1e-10 * scale
-    assert np.abs(V[0] - fo.V[:, :K + 1]).max() <= 1e-8
+    # V carries the loss-of-orthogonality noise (~sqrt(eps) just before each redo)
+    assert np.abs(V[0] - fo.V[:, :K + 1]).max() <= 1e-7
     # (4) free-running oracle: same decisions away from the threshold band
     ff = O.Factor(csc, bs[0], K)
     for j in range(1, K + 1):
         lo, re = ff.lanczos_reorth(j)
         if re != flags[j - 1]:
-            assert thr / 2 < lo < 2 * thr, (j, lo)
+            assert thr / 10 < lo < 10 * thr, (j, lo)
             break
 
 
