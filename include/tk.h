@@ -7,6 +7,9 @@
  * tk_status (0 = TK_OK); on failure tk_last_error() (thread-local) says why.  Nothing
  * throws or aborts across this boundary.  A tk_ctx is externally synchronised (one
  * host thread at a time), exactly like the reference's single-threaded Julia driver.
+ * Handles may be destroyed in any order (garbage-collector finalizers): a matrix keeps
+ * its context alive and a decomposition keeps its context and matrices alive until it
+ * is destroyed itself.
  *
  * Conventions
  *   - fp64 throughout (the reference is Float64 everywhere).

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -67,6 +68,9 @@ struct tk_ctx {
     long cnt[TCLS_N] = {0};
     double* xbuf = nullptr;   // host-allreduce staging
     size_t xcap = 0;
+    // Handles may be destroyed in any order (Julia finalizers, Python GC): matrices and
+    // decompositions hold a reference on their context, decompositions on their matrices.
+    std::atomic<int> refs{1};
 };
 
 struct Timer {
@@ -135,8 +139,8 @@ tk_status tk_ctx_create(int device, tk_ctx** out) {
     return TK_OK;
 }
 
-tk_status tk_ctx_destroy(tk_ctx* c) {
-    if (!c) return TK_OK;
+static void ctx_release(tk_ctx* c) {
+    if (--c->refs > 0) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->xstream);
@@ -146,6 +150,11 @@ tk_status tk_ctx_destroy(tk_ctx* c) {
     hipStreamDestroy(c->stream);
     hipStreamDestroy(c->xstream);
     delete c;
+}
+
+tk_status tk_ctx_destroy(tk_ctx* c) {
+    if (!c) return TK_OK;
+    ctx_release(c);
     return TK_OK;
 }
 
@@ -199,6 +208,7 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) {
 // ------------------------------------------------------------------ matrices
 struct tk_mat {
     tk_ctx* ctx;
+    std::atomic<int> refs{1};
     int64_t n = 0, nnz = 0;
     int* rowptr = nullptr;
     int* col = nullptr;
@@ -365,6 +375,7 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
         free_mat(A);
         return fail(TK_ERR_ALLOC, "matrix upload: %s", hipGetErrorString(e));
     }
+    c->refs++;
     *out = A;
     return TK_OK;
 }
@@ -423,10 +434,18 @@ tk_status tk_matrix_from_csr(tk_ctx* c, int64_t n, const int64_t* rowptr, const 
     return upload_csr(c, n, rp, ci, v, out);
 }
 
+static void mat_release(tk_mat* A) {
+    if (--A->refs > 0) return;
+    tk_ctx* c = A->ctx;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    free_mat(A);
+    ctx_release(c);
+}
+
 tk_status tk_matrix_destroy(tk_mat* A) {
     if (!A) return TK_OK;
-    hipSetDevice(A->ctx->device);
-    free_mat(A);
+    mat_release(A);
     return TK_OK;
 }
 
@@ -593,15 +612,22 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
     }
+    c->refs++;
+    for (tk_mat* A : dc->mats) A->refs++;
     *out = dc;
     return TK_OK;
 }
 
 tk_status tk_decomp_destroy(tk_decomp* dc) {
     if (!dc) return TK_OK;
-    hipSetDevice(dc->ctx->device);
-    hipStreamSynchronize(dc->ctx->stream);
+    tk_ctx* c = dc->ctx;
+    std::vector<tk_mat*> mats = dc->mats;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(c->xstream);
     free_decomp(dc);
+    for (tk_mat* A : mats) mat_release(A);
+    ctx_release(c);
     return TK_OK;
 }
 

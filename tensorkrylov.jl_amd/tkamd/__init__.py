@@ -8,10 +8,12 @@ hand-written gfx950 kernels run the per-factor Krylov steps and V*Y.
 from ._lib import TKError, lib  # noqa: F401
 from .compressed import (ApproximationData, CompressedNormBreakdown, SpectralData,  # noqa: F401
                          residualnorm, solve_compressed_system)
-from .decompositions import (METHODS, Partition, TensorArnoldi, TensorDecomposition,  # noqa: F401
-                             TensorLanczos, TensorLanczosReorth)
+from .decompositions import (METHODS, Decomposition, Partition, TensorArnoldi,  # noqa: F401
+                             TensorDecomposition, TensorLanczos, TensorLanczosReorth,
+                             arnoldi_algorithm, isorthonormal, lanczos_algorithm,
+                             orthogonality_loss)
 from .device import Context, DeviceDecomposition, DeviceMatrix, unique_id  # noqa: F401
 from .solver import solve_tensorized_system, tensorkrylov  # noqa: F401
 from .structures import (ConvDiff, ConvergenceData, KroneckerMatrix, KruskalTensor,  # noqa: F401
                          Laplace, NonSymInstance, RandSparseSPD, SymInstance, TensorizedSystem,
-                         assemble_matrix, normalize_rhs, random_rhs)
+                         as_csc, assemble_matrix, normalize_rhs, random_rhs)

@@ -182,3 +182,72 @@ class TensorLanczosReorth(TensorDecomposition):
 
 METHODS = {"TensorArnoldi": TensorArnoldi, "TensorLanczos": TensorLanczos,
            "TensorLanczosReorth": TensorLanczosReorth}
+
+
+# ------------------------------------------------------------------ single-matrix drivers
+class Decomposition:
+    """Result of arnoldi_algorithm / lanczos_algorithm: the reference's Arnoldi / Lanczos
+    structs (src/decompositions.jl:28-110) with host copies of V and H."""
+
+    def __init__(self, A, V, H, loss=None):
+        self.A, self.V, self.H = A, V, H
+        self.loss = loss
+
+
+def _single(cls, A, b, nmax, ctx, backend):
+    from .structures import KroneckerMatrix, SymInstance, as_csc
+    csc = as_csc(A)
+    td = cls(KroneckerMatrix(SymInstance, [csc]), nmax, ctx=ctx, track_all_gram=True, backend=backend)
+    return td, csc
+
+
+def arnoldi_algorithm(A, b, k, ctx=None, backend=None):
+    """arnoldi_algorithm(A, b, k) (src/orthogonal_bases.jl:182-195): k Arnoldi steps from
+    V[:,1] = b/|b|; V is n x (k+1), H is (k+1) x k."""
+    td, csc = _single(TensorArnoldi, A, b, k, ctx, backend)
+    try:
+        td.orthonormalize_first([b])
+        for j in range(2, k + 1):
+            td.orthonormalize(j)
+        td.flush()
+        return Decomposition(csc, td.basis(0, k + 1), td.H[0, :k + 1, :k].copy())
+    finally:
+        td.close()
+
+
+def lanczos_algorithm(A, b, k, reorth=False, ctx=None, backend=None):
+    """lanczos_algorithm(A, b, k[, LanczosReorth]) (src/orthogonal_bases.jl:198-229): k-1
+    three-term steps; V is n x k, H is k x k (H[k,k] is left 0 as in the reference)."""
+    if k < 2:
+        raise ValueError("lanczos_algorithm needs k >= 2")
+    cls = TensorLanczosReorth if reorth else TensorLanczos
+    td, csc = _single(cls, A, b, k - 1, ctx, backend)
+    try:
+        td.orthonormalize_first([b])
+        for j in range(2, k):
+            td.orthonormalize(j)
+        td.flush()
+        H = td.H[0, :k, :k].copy()
+        H[k - 1, k - 1] = 0.0
+        return Decomposition(csc, td.basis(0, k), H, td.loss[0, :k - 1].copy() if reorth else None)
+    finally:
+        td.close()
+
+
+def orthogonality_loss(V, k):
+    """norm(V[:,1:k]'V[:,1:k] - I) (src/orthogonal_bases.jl:250-257)."""
+    Vk = np.asarray(V)[:, :k]
+    return float(np.linalg.norm(Vk.T @ Vk - np.eye(k)))
+
+
+def isorthonormal(x, k, tol=1e-8):
+    """isorthonormal(V | decomposition | tensor decomposition, k) (src/orthogonal_bases.jl:
+    259-284).  A TensorDecomposition is checked through the device Gram rows of every factor
+    it tracks (all factors when built with track_all_gram=True)."""
+    if isinstance(x, Decomposition):
+        return orthogonality_loss(x.V, k) < tol
+    if isinstance(x, TensorDecomposition):
+        if not x.gram:
+            raise ValueError("no Gram rows tracked for this decomposition")
+        return all(x.orthogonality_loss(s, k) < tol for s in x.gram)
+    return orthogonality_loss(x, k) < tol

@@ -92,6 +92,30 @@ def rand_sparse_spd(n, seed=42, nnz_row=15):
     return colptr, rows.astype(np.int64), vals
 
 
+def as_csc(A):
+    """0-based (colptr, rowval, nzval) of a CSC triple, a scipy.sparse matrix or a dense
+    array (explicit zeros of a dense input are dropped, as sparse() does in Julia)."""
+    if isinstance(A, tuple) and len(A) == 3:
+        return (np.ascontiguousarray(A[0], dtype=np.int64), np.ascontiguousarray(A[1], dtype=np.int64),
+                np.ascontiguousarray(A[2], dtype=np.float64))
+    if hasattr(A, "tocsc"):
+        S = A.tocsc()
+        S.sort_indices()
+        return (S.indptr.astype(np.int64), S.indices.astype(np.int64), S.data.astype(np.float64))
+    D = np.asarray(A, dtype=np.float64)
+    if D.ndim != 2 or D.shape[0] != D.shape[1]:
+        raise ValueError("A must be square")
+    n = D.shape[0]
+    colptr = np.zeros(n + 1, dtype=np.int64)
+    rows, vals = [], []
+    for j in range(n):
+        nzr = np.nonzero(D[:, j])[0]
+        rows.append(nzr)
+        vals.append(D[nzr, j])
+        colptr[j + 1] = colptr[j] + len(nzr)
+    return colptr, np.concatenate(rows).astype(np.int64), np.concatenate(vals)
+
+
 def csc_leading_block(csc, k):
     """Dense A[1:k, 1:k] of a CSC matrix (for spectral data of non-Laplace classes,
     src/eigenvalues.jl:337,344-350)."""

@@ -223,3 +223,44 @@ def test_driver_host_logic_matches_oracle(method, cls, sym, d, K):
     ref = np.array(conv_o.relative_residual_norm)
     assert np.abs(conv.relative_residual_norm - ref).max() <= 1e-12 * ref.max()
     assert np.allclose(conv.orthogonality_data[1:], conv_o.orthogonality_data[1:], rtol=1e-6, atol=1e-15)
+
+
+# ------------------------------------------------------------------ single-matrix drivers (a12)
+def test_single_matrix_drivers_host_logic():
+    """arnoldi_algorithm / lanczos_algorithm / isorthonormal (src/orthogonal_bases.jl:182-284)
+    over the CPU stand-in: shapes and H/V follow the reference structs; test/decompositions.jl:4-19
+    properties."""
+    from _fake_device import backend
+    n, k = 300, 40
+    A = O.laplace_dense(n)
+    b = np.random.default_rng(7).random(n)
+    ar = tkamd.arnoldi_algorithm(A, b, k, backend=backend)
+    assert ar.V.shape == (n, k + 1) and ar.H.shape == (k + 1, k)
+    f = O.Factor(O.dense_to_csc(A), b, k)
+    for j in range(1, k + 1):
+        f.arnoldi_mgs(j)
+    assert np.array_equal(ar.H, f.H[:k + 1, :k]) and np.array_equal(ar.V, f.V[:, :k + 1])
+    assert tkamd.isorthonormal(ar, k)
+    la = tkamd.lanczos_algorithm(A, b, k, backend=backend)
+    assert la.V.shape == (n, k) and la.H.shape == (k, k) and la.H[k - 1, k - 1] == 0.0
+    assert tkamd.isorthonormal(la, k - 1)
+    assert np.all(np.linalg.eigvalsh(la.H[:k - 1, :k - 1]) > 0)
+    assert not tkamd.isorthonormal(np.ones((n, 3)), 3)
+
+
+def test_as_csc_inputs():
+    A = O.convdiff_dense(50)
+    ref = O.dense_to_csc(A)
+    import scipy.sparse as sp
+    for x in (tkamd.as_csc(A), tkamd.as_csc(sp.csr_matrix(A)), tkamd.as_csc(ref)):
+        for u, v in zip(x, ref):
+            assert np.array_equal(u, v)
+
+
+def test_handles_destroyed_in_any_order_without_gpu():
+    """Destroy entry points accept NULL and never crash (the refcounted order-independence
+    itself is exercised on the GPU by test_gpu_parity's session teardown)."""
+    lib = L.lib()
+    assert lib.tk_decomp_destroy(None) == 0
+    assert lib.tk_matrix_destroy(None) == 0
+    assert lib.tk_ctx_destroy(None) == 0
