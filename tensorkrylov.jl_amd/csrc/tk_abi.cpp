@@ -561,7 +561,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     for (int f = 0; f < nf; ++f) {
         DFac& d = dc->hf[f];
         d.A = mats[f]->spm();
-        DA(d.V, (size_t)dc->ntiles * 256 * KC * sizeof(double));   // tile-major
+        DA(d.V, (size_t)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double));   // tile-major, paired columns
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
         hipError_t e = hipMemcpy(bb, b[f], n * sizeof(double), hipMemcpyHostToDevice);

@@ -2,13 +2,15 @@
 // thbake/TensorKrylov.jl.
 //
 // Layout (DESIGN.md "Data layout in HBM"): the basis V_s of every factor is stored
-// TILE-MAJOR: rows are cut into 256-row tiles and each tile holds its kmax+1 columns
-// contiguously, element (r, c) at  (r/256)*256*(kmax+1) + c*256 + r%256.  A 256-thread
-// block owns one tile at a time; thread t keeps its row V[r, 0..ncols) in VGPRs,
-// loaded with buffer_load_dwordx2 whose hardware range check (num_records =
-// ncols*2 KiB from the tile base) zero-fills the columns a step does not use -- no
-// per-column predicates, one 32-bit VGPR offset per load, and a whole tile's columns
-// inside one 2 MiB page.  All n-length vectors are padded to whole tiles (zeros).
+// TILE-MAJOR with PAIRED COLUMNS: rows are cut into 256-row tiles; a tile holds its
+// KCP = kmax+1 rounded up to even columns contiguously, as column pairs, element (r, c) at
+//   (r/256)*256*KCP + (c/2)*512 + (r%256)*2 + c%2.
+// A 256-thread block owns one tile at a time; thread t keeps its row V[r, 0..ncols) in
+// VGPRs, loaded two columns per buffer_load_dwordx4 (1 KiB per wave instruction; measured
+// 6.0 TB/s vs 5.6 with one column per dwordx2, tools/bwprobe.hip) whose hardware range
+// check (num_records = whole column pairs from the tile base) zero-fills the pairs a step
+// does not use; the odd column of a half-used pair is cleared in registers.  All
+// n-length vectors are padded to whole tiles (zeros).
 //
 // Numerical scheme (DESIGN.md "Arnoldi step"): the reference's two-pass MGS
 // (src/orthogonal_bases.jl:15-37) is computed as CGS2 -- h1 = V'w, w' = w - V h1,
@@ -27,6 +29,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tk_internal.h"
 
 namespace tk {
@@ -34,6 +38,14 @@ namespace tk {
 #define TPB 256          // threads per block == rows per tile
 #define CH 16            // values per block-reduction chunk
 #define TSTR (TPB + 16)  // LDS stride (doubles) of the transpose buffer
+// Occupancy of the streaming pass kernels (waves per SIMD, by register-row width): the
+// compiler's own choice left 40/56-column rows at one wave less than their registers
+// allow; these limits are the largest that compile without spills.
+#define OCC_WAVES(L4, L3) (MAXC <= (L4) ? 4 : (MAXC <= (L3) ? 3 : 2))
+// SpMV-fused kernels: the gather formats need more registers
+#define A1_L4(F) ((F) == 1 || (F) == 3 ? 40 : ((F) == 2 ? 24 : 16))
+#define A1_L3(F) ((F) == 1 || (F) == 3 ? 56 : ((F) == 2 ? 40 : 32))
+#define OCC_ATTR(L4, L3) __attribute__((amdgpu_waves_per_eu(OCC_WAVES(L4, L3), OCC_WAVES(L4, L3))))
 #define COEF_PAD(kmax) ((kmax) + 2 > 64 ? (kmax) + 2 : 64)   // LDS coefficient array length
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -44,9 +56,23 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 __device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
 }
+// V is streamed once per pass and never re-read from cache within a step: non-temporal
+// loads (aux = 2, `nt`) measured 3-5 % faster than the default policy (tools/bwprobe.hip).
 __device__ __forceinline__ double bld(rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2));
 }
+
+typedef double d2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ d2_t bld2(rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(d2_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+}
+// Paired-column tile layout: element offset of (row t, column c) inside a tile, byte
+// offset of column c relative to thread t's pair base (t*16), tile stride, and the
+// range-check size that admits columns [0, nc).
+__device__ __forceinline__ int64_t vofs(int c, int t) { return ((int64_t)(c >> 1) * TPB + t) * 2 + (c & 1); }
+__device__ __forceinline__ uint32_t cofs(int c) { return (uint32_t)(c >> 1) * (TPB * 16) + (uint32_t)(c & 1) * 8; }
+__host__ __device__ __forceinline__ int kcp(int kmax) { return (kmax + 2) & ~1; }
+__device__ __forceinline__ uint32_t vrange(int nc) { return (uint32_t)((nc + 1) >> 1) * (TPB * 16); }
 
 // Julia's CSC scatter adds nz*x into y without FMA; keep products and sums separately
 // rounded so the device SpMV equals it bit for bit (__dmul_rn/__dadd_rn are plain
@@ -94,16 +120,28 @@ __device__ __forceinline__ void chunk_reduce(const double (&x)[CH], double* __re
     __syncthreads();
 }
 
-// Row of V held in VGPRs: v[c] = V[r, c] for c < MAXC (zero for c >= the range the
-// tile resource admits).
+// Row of V held in VGPRs: v[c] = V[r, c] for c < MAXC, zero for c >= nc (pairs beyond
+// the resource's range read as zero; the odd half of the last pair is cleared here).
 template <int MAXC>
 struct Row {
+    static_assert(MAXC % 2 == 0, "register rows hold whole column pairs");
     double v[MAXC];
-    __device__ __forceinline__ void load(rsrc_t tile, uint32_t toff) {
+    __device__ __forceinline__ void load(rsrc_t tile, uint32_t toff, int nc) {
 #pragma unroll
-        for (int c = 0; c < MAXC; ++c) v[c] = bld(tile, toff + (uint32_t)c * (TPB * 8));
+        for (int p = 0; p < MAXC / 2; ++p) {
+            const d2_t x = bld2(tile, toff + (uint32_t)p * (TPB * 16));
+            v[2 * p] = x.x;
+            v[2 * p + 1] = 2 * p + 1 < nc ? x.y : 0.0;
+        }
     }
 };
+
+// Store V[r, c] as a whole 16-byte column pair (`other` = the pair's other column): a lone
+// 8-byte store would leave half-written 32-byte sectors behind.
+__device__ __forceinline__ void st_pair(double* V, int64_t tile_base, int c, int t, double v, double other) {
+    const d2_t x = (c & 1) ? (d2_t){other, v} : (d2_t){v, other};
+    GP(d2_t, V + tile_base + vofs(c & ~1, t))[0] = x;
+}
 
 // sum_c V[r,c] * h[c] for c < nc.  h is in LDS (broadcast reads) and zero-padded to
 // MAXC, and R.v[c] is zero for c >= nc (range-checked load): no per-column conditions.
@@ -113,41 +151,53 @@ __device__ __forceinline__ double row_dot(const Row<MAXC>& R, rsrc_t tile, uint3
     double s = 0.0;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) s += R.v[c] * h[c];
-    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + (uint32_t)c * (TPB * 8)) * h[c];
+    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + cofs(c)) * h[c];
     return s;
 }
 
 // Block-reduce V[r,i]*y for i < lim (lim == the row's loaded column count, so R.v[i]
 // is zero beyond it) into acc[base .. base+lim).  Entries up to base+roundup16(lim)
-// receive zeros (callers reduce extra scalars into them afterwards).
+// receive zeros (callers reduce extra scalars into them afterwards).  MAXC need not be a
+// multiple of CH: the rest of the last register chunk is streamed (range-checked zeros).
 template <int MAXC>
 __device__ __forceinline__ void reduce_row(const Row<MAXC>& R, rsrc_t tile, uint32_t toff, int lim,
                                            double y, double* tr, double* acc, int base, bool first) {
+    constexpr int MR = (MAXC + CH - 1) / CH * CH;
 #pragma unroll
-    for (int c0 = 0; c0 < MAXC; c0 += CH) {
+    for (int c0 = 0; c0 < MR; c0 += CH) {
         if (c0 < lim) {
             double x[CH];
 #pragma unroll
-            for (int q = 0; q < CH; ++q) x[q] = R.v[c0 + q] * y;
+            for (int q = 0; q < CH; ++q)
+                x[q] = (c0 + q < MAXC ? R.v[c0 + q < MAXC ? c0 + q : 0]
+                                      : (c0 + q < lim ? bld(tile, toff + cofs(c0 + q)) : 0.0)) * y;
             chunk_reduce(x, tr, acc, base + c0, first);
         }
     }
-    for (int c0 = MAXC; c0 < lim; c0 += CH) {
+    for (int c0 = MR; c0 < lim; c0 += CH) {
         double x[CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) x[q] = bld(tile, toff + (uint32_t)(c0 + q) * (TPB * 8)) * y;
+        for (int q = 0; q < CH; q += 2) {
+            const d2_t p = bld2(tile, toff + cofs(c0 + q));
+            x[q] = p.x * y;
+            x[q + 1] = (c0 + q + 1 < lim ? p.y : 0.0) * y;
+        }
         chunk_reduce(x, tr, acc, base + c0, first);
     }
 }
 
 // Same without a register row (streams V[r, 0..lim) from the tile; the tile resource
-// must admit exactly lim columns).
+// must admit the pairs of exactly lim columns).
 __device__ __forceinline__ void reduce_stream(rsrc_t tile, uint32_t toff, int lim, double y, double* tr,
                                               double* acc, int base, bool first) {
     for (int c0 = 0; c0 < lim; c0 += CH) {
         double x[CH];
 #pragma unroll
-        for (int q = 0; q < CH; ++q) x[q] = bld(tile, toff + (uint32_t)(c0 + q) * (TPB * 8)) * y;
+        for (int q = 0; q < CH; q += 2) {
+            const d2_t p = bld2(tile, toff + cofs(c0 + q));
+            x[q] = p.x * y;
+            x[q + 1] = (c0 + q + 1 < lim ? p.y : 0.0) * y;
+        }
         chunk_reduce(x, tr, acc, base + c0, first);
     }
 }
@@ -227,7 +277,7 @@ __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
     __shared__ double tr[CH * TSTR];                                   \
     extern __shared__ __attribute__((aligned(16))) double lds[];       \
     const DFac& d = F[blockIdx.y];                                     \
-    const int64_t TS = (int64_t)TPB * (a.kmax + 1);                    \
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);                     \
     (void)TS;
 
 #define TILE_LOOP                                                                  \
@@ -236,7 +286,7 @@ __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
         const int64_t r = (int64_t)tile * TPB + threadIdx.x;                       \
         const bool ok = r < a.n;                                                   \
         const double* Vt = d.V + (int64_t)tile * TS;                               \
-        const uint32_t toff = threadIdx.x * 8u;                                    \
+        const uint32_t toff = threadIdx.x * 16u;                                   \
         (void)Vt; (void)toff; (void)ok;
 
 // ------------------------------------------------------------------ init kernels
@@ -262,7 +312,7 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
     TILE_LOOP
         const double bv = ld(d.b, r);
         const double v0 = inv * bv;
-        st(d.V, (int64_t)tile * TS + threadIdx.x, v0);
+        st_pair(d.V, (int64_t)tile * TS, 0, threadIdx.x, v0, 0.0);   // column 1 not yet written
         const double e[2] = {v0 * bv, v0 * v0};
         reduce_scalars<2>(e, tr, acc, 0, first);
     }
@@ -273,16 +323,16 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 
 // First pass, v_j stored:  W = A v_j;  P1 = [ <V[:,c], W>, c = 0..j ].
 template <int MAXC, int FMT>
-__global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1_plain(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     double* acc = lds;
     const int j = a.j, nc = j + 1;
     TILE_LOOP
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
+        const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
-        R.load(tv, toff);
+        R.load(tv, toff, nc);
         const double* Vg = d.V;
-        const double w = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
+        const double w = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + vofs(j, (int)(c & 255))); }) : 0.0;
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, nc, w, tr, acc, 0, first);
     }
@@ -294,7 +344,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_plain(const DFac* __restrict__ F
 //   W   = (A U - V[:,0..j) g[0..j) - g[j] v_j) * inv_beta    (= A v_j, Arnoldi relation)
 //   P1  = [ <V[:,c],W> (c<j), <v_j,W> ]
 template <int MAXC, int FMT>
-__global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j;
     const int CP = COEF_PAD(a.kmax);
@@ -307,15 +357,15 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F
     const double inv_beta = ld(d.sc, SC_INVBETA);
     const double gj = ld(d.g, j);
     TILE_LOOP
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)j * TPB * 8);
+        const rsrc_t tv = mkrsrc(Vt, vrange(j));
         Row<MAXC> R;
-        R.load(tv, toff);
+        R.load(tv, toff, j);
         const double* Ug = d.U;
         const double au = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double w = ok ? (au - row_dot(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
-        st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
+        st_pair(d.V, (int64_t)tile * TS, j, threadIdx.x, vj, (j & 1) ? bld(tv, toff + cofs(j - 1)) : 0.0);
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, j, w, tr, acc, 0, first);
         const double e1[1] = {vj * w};
@@ -328,7 +378,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a1_fused(const DFac* __restrict__ F
 // (both need only V[r, 0..j], already in registers):
 //   P2 = [ <V[:,c],U> (c<=j), <U,U>, <v_j,b> | gram <V[:,c],v_j> (c<=j) ]
 template <int MAXC>
-__global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) OCC_ATTR(32, 56) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
     const int CP = COEF_PAD(a.kmax);
@@ -338,10 +388,10 @@ __global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArg
     __syncthreads();
     const bool gram = d.track_gram != 0;
     TILE_LOOP
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
+        const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
-        R.load(tv, toff);
-        const double vj = bld(tv, toff + (uint32_t)j * (TPB * 8));
+        R.load(tv, toff, nc);
+        const double vj = bld(tv, toff + cofs(j));
         const double w = ld(d.W, r);
         const double u = ok ? (w - row_dot(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
@@ -356,7 +406,7 @@ __global__ __launch_bounds__(TPB) void k_arn_a2(const DFac* __restrict__ F, KArg
 // Write the pending column j+1 with no following step:
 //   v = (U - V[:,0..j] h2) * inv_beta;  P1 = [ gram <V[:,c],v> (c<=j), <v,v>, <v,b> ]
 template <int MAXC>
-__global__ __launch_bounds__(TPB) void k_arn_finalize(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
     const int CP = COEF_PAD(a.kmax);
@@ -366,12 +416,12 @@ __global__ __launch_bounds__(TPB) void k_arn_finalize(const DFac* __restrict__ F
     __syncthreads();
     const double inv_beta = ld(d.sc, SC_INVBETA);
     TILE_LOOP
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
+        const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
-        R.load(tv, toff);
+        R.load(tv, toff, nc);
         const double up = ld(d.U, r);
         const double v = ok ? (up - row_dot(R, tv, toff, nc, h2)) * inv_beta : 0.0;
-        st(d.V, (int64_t)tile * TS + (int64_t)(j + 1) * TPB + threadIdx.x, v);
+        st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? bld(tv, toff + cofs(j)) : 0.0);
         reduce_row<MAXC>(R, tv, toff, nc, v, tr, acc, 0, first);
         const double e[2] = {v * v, v * ld(d.b, r)};
         reduce_scalars<2>(e, tr, acc, nc, first);
@@ -392,10 +442,10 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_plain(const DFac* __restrict__ F
     const double bp = j > 0 ? ld(d.sc, SC_BETAPREV) : 0.0;
     TILE_LOOP
         const double* Vg = d.V;
-        const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + (int64_t)j * TPB + (c & 255)); }) : 0.0;
-        const double prev = j > 0 ? ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x) : 0.0;
+        const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + vofs(j, (int)(c & 255))); }) : 0.0;
+        const double prev = j > 0 ? ld(Vt, vofs(j - 1, threadIdx.x)) : 0.0;
         const double u = av - bp * prev;
-        const double v = ld(Vt, (int64_t)j * TPB + threadIdx.x);
+        const double v = ld(Vt, vofs(j, threadIdx.x));
         st(d.U, r, u);
         const double e[1] = {u * v};
         reduce_scalars<1>(e, tr, acc, 0, first);
@@ -420,10 +470,11 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F
         const double vj = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
         const double* Wg = d.W;
         const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return zero ? 0.0 : mul_rn(ld(Wg, c), inv_beta); }) : 0.0;
-        const double u = av - beta * ld(Vt, (int64_t)(j - 1) * TPB + threadIdx.x);
-        st(d.V, (int64_t)tile * TS + (int64_t)j * TPB + threadIdx.x, vj);
+        const double vprev = ld(Vt, vofs(j - 1, threadIdx.x));
+        const double u = av - beta * vprev;
+        st_pair(d.V, (int64_t)tile * TS, j, threadIdx.x, vj, (j & 1) ? vprev : 0.0);
         st(d.U, r, u);
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)j * TPB * 8);
+        const rsrc_t tv = mkrsrc(Vt, vrange(j));
         const double e1[2] = {u * vj, vj * ld(d.b, r)};
         reduce_scalars<2>(e1, tr, acc, 0, first);
         if (gram) {
@@ -443,7 +494,7 @@ __global__ __launch_bounds__(TPB) void k_lan_l2(const DFac* __restrict__ F, KArg
     const int j = a.j;
     const double alpha = ld(d.RED1, 0);
     TILE_LOOP
-        const double w = ok ? ld(d.U, r) - alpha * ld(Vt, (int64_t)j * TPB + threadIdx.x) : 0.0;
+        const double w = ok ? ld(d.U, r) - alpha * ld(Vt, vofs(j, threadIdx.x)) : 0.0;
         st(d.W, r, w);
         const double e[1] = {w * w};
         reduce_scalars<1>(e, tr, acc, 0, first);
@@ -464,8 +515,8 @@ __global__ __launch_bounds__(TPB) void k_lan_finalize(const DFac* __restrict__ F
     const bool gram = d.track_gram != 0;
     TILE_LOOP
         const double v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
-        st(d.V, (int64_t)tile * TS + (int64_t)(j + 1) * TPB + threadIdx.x, v);
-        const rsrc_t tv = mkrsrc(Vt, (uint32_t)nc * TPB * 8);
+        st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? ld(Vt, vofs(j, threadIdx.x)) : 0.0);
+        const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         const double e1[1] = {v * ld(d.b, r)};
         reduce_scalars<1>(e1, tr, acc, 0, first);
         if (gram) {
@@ -633,19 +684,23 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // blockIdx.y; X column-major with leading dimension ld.  Block = one 256-row tile;
 // wave w owns rows 64w..64w+63 as 4 strips of 16; NG 16-column groups per launch
 // (blockIdx.z walks further groups).  v_mfma_f64_16x16x4_f64 with
-//   A = V[16 rows x 4 cols]  lane l: row l&15, col l>>4 (tile buffer load, range-checked)
-//   B = Y[4 x 16]            lane l: row l>>4, col l&15 (LDS)
-//   D                        lane l: row (l>>4) + 4i, col l&15
+//   A = V[16 rows x 4 k]  lane l: row l&15, k-slot l>>4
+//   B = Y[4 k x 16]       lane l: k-slot l>>4, col l&15 (LDS)
+//   D                     lane l: row (l>>4) + 4i, col l&15
+// The sum over k is order-free, so the k-slots are permuted to match the paired-column
+// layout: one dwordx4 per lane fetches V[row, 2m..2m+1] (m = kk/2 + slot) and feeds two
+// MFMAs, the first over columns kk + 2*slot, the second over kk + 2*slot + 1.
 // Each D register store covers 4 consecutive rows of 16 columns; the four registers
 // of a strip complete 16-row runs that the L2 merges before write-back.
+#define YS_STRIDE 72   // LDS row stride of Ys: rows 2*slot apart land 32 banks apart
 template <int NG>
 __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
                                                    const double* __restrict__ Yall,
                                                    double* __restrict__ Xall, int k, int t) {
-    __shared__ double Ys[64 * 80];   // [kk][col] of one 64-deep k chunk (stride 80: conflict-free)
+    __shared__ double Ys[64 * YS_STRIDE];   // [kk][col] of one 64-deep k chunk
     const int f = blockIdx.y;
     const DFac& d = F[f];
-    const int64_t TS = (int64_t)TPB * (a.kmax + 1);
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     const double* Y = Yall + (int64_t)f * k * t;
     double* X = Xall + (int64_t)f * a.ld * t;
     const int tile = blockIdx.x;
@@ -664,23 +719,30 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
         __syncthreads();
         for (int i = threadIdx.x; i < 64 * 16 * NG; i += 256) {
             const int kk = i & 63, tt = i >> 6;
-            Ys[kk * 80 + tt] = (kk < kn && tt < tn) ? ld(Y, (int64_t)(t0 + tt) * k + k0 + kk) : 0.0;
+            Ys[kk * YS_STRIDE + tt] = (kk < kn && tt < tn) ? ld(Y, (int64_t)(t0 + tt) * k + k0 + kk) : 0.0;
         }
         __syncthreads();
-        const rsrc_t tv = mkrsrc(Vt + (int64_t)k0 * TPB, (uint32_t)kn * TPB * 8);
-        const int kp = (kn + 3) & ~3;
-        for (int kk = 0; kk < kp; kk += 4) {
-            const int ka = kk + lk;
-            double bq[NG];
+        const rsrc_t tv = mkrsrc(Vt + (int64_t)k0 * TPB, vrange(kn));   // k0 is even: pair aligned
+        const int kp = (kn + 7) & ~7;
+        for (int kk = 0; kk < kp; kk += 8) {
+            const int ka = kk + 2 * lk;   // this lane's first column of the pair
+            double bq0[NG], bq1[NG];
 #pragma unroll
-            for (int q = 0; q < NG; ++q) bq[q] = Ys[ka * 80 + 16 * q + lr];
+            for (int q = 0; q < NG; ++q) {
+                bq0[q] = Ys[ka * YS_STRIDE + 16 * q + lr];
+                bq1[q] = Ys[(ka + 1) * YS_STRIDE + 16 * q + lr];
+            }
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int row = wave * 64 + s * 16 + lr;
-                const double av = bld(tv, (uint32_t)(ka * TPB + row) * 8u);
+                const d2_t av = bld2(tv, ((uint32_t)(ka >> 1) * TPB + row) * 16u);
+                const double a1 = ka + 1 < kn ? av.y : 0.0;   // odd column past k: stale data
 #pragma unroll
                 for (int q = 0; q < NG; ++q)
-                    acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bq[q], acc[s][q], 0, 0, 0);
+                    acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bq0[q], acc[s][q], 0, 0, 0);
+#pragma unroll
+                for (int q = 0; q < NG; ++q)
+                    acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bq1[q], acc[s][q], 0, 0, 0);
             }
         }
     }
@@ -710,10 +772,10 @@ __global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ 
 // out[c*n + r] = V[r, c0 + c] for one factor (column extraction for the ABI)
 __global__ __launch_bounds__(TPB) void k_get_cols(const double* __restrict__ V, int64_t n, int kmax,
                                                   int c0, int nc, double* __restrict__ out) {
-    const int64_t TS = (int64_t)TPB * (kmax + 1);
+    const int64_t TS = (int64_t)TPB * kcp(kmax);
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
     const int c = blockIdx.y;
-    if (r < n && c < nc) st(out, (int64_t)c * n + r, ld(V, (r >> 8) * TS + (int64_t)(c0 + c) * TPB + (r & 255)));
+    if (r < n && c < nc) st(out, (int64_t)c * n + r, ld(V, (r >> 8) * TS + vofs(c0 + c, (int)(r & 255))));
 }
 
 // ------------------------------------------------------------------ launchers
@@ -722,17 +784,32 @@ static size_t lds_bytes(int nv, int kmax, int ncoef) {
     return (size_t)(ncoef * COEF_PAD(kmax) + ((nv + 32 + 15) & ~15)) * sizeof(double);
 }
 
-#define DISPATCH_MAXC(ncols, KERNEL, ...)                  \
-    do {                                                   \
-        if ((ncols) <= 16)                                 \
-            hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__);   \
-        else if ((ncols) <= 32)                            \
-            hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__);   \
-        else if ((ncols) <= 48)                            \
-            hipLaunchKernelGGL(KERNEL<48>, __VA_ARGS__);   \
-        else                                               \
-            hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__);   \
-    } while (0)
+// The register row is sized to the step's column count in steps of 8: out-of-range
+// columns cost a load issue each even though the range check fetches nothing, and the
+// unused registers lower occupancy (tools/bwprobe.hip: 12 columns with a 48-register row
+// streamed at 3.5 TB/s, with a 16-register row at 5.6 TB/s).
+template <int V>
+using IC = std::integral_constant<int, V>;
+template <class F>
+static void with_maxc(int nc, F f) {
+    if (nc <= 8) f(IC<8>{});
+    else if (nc <= 16) f(IC<16>{});
+    else if (nc <= 24) f(IC<24>{});
+    else if (nc <= 32) f(IC<32>{});
+    else if (nc <= 40) f(IC<40>{});
+    else if (nc <= 48) f(IC<48>{});
+    else if (nc <= 56) f(IC<56>{});
+    else f(IC<64>{});
+}
+template <class F>
+static void with_fmt(int fmt, F f) {
+    switch (fmt) {
+        case SPM_DIA: f(IC<SPM_DIA>{}); break;
+        case SPM_SELL: f(IC<SPM_SELL>{}); break;
+        case SPM_CSR: f(IC<SPM_CSR>{}); break;
+        default: f(IC<SPM_ANY>{}); break;
+    }
+}
 
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_init_a, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
@@ -740,53 +817,47 @@ void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_init_b, dim3(a.npart, nf), dim3(TPB), lds_bytes(2, a.kmax, 0), s, F, a);
 }
-#define DISPATCH_FMT_MAXC(fmt, ncols, KERNEL, ...)                                  \
-    do {                                                                            \
-        switch (fmt) {                                                              \
-            case SPM_DIA: DISPATCH_MAXC2(ncols, KERNEL, SPM_DIA, __VA_ARGS__); break;   \
-            case SPM_SELL: DISPATCH_MAXC2(ncols, KERNEL, SPM_SELL, __VA_ARGS__); break; \
-            case SPM_CSR: DISPATCH_MAXC2(ncols, KERNEL, SPM_CSR, __VA_ARGS__); break;   \
-            default: DISPATCH_MAXC2(ncols, KERNEL, SPM_ANY, __VA_ARGS__); break;        \
-        }                                                                           \
-    } while (0)
-#define DISPATCH_MAXC2(ncols, KERNEL, F_, ...)                   \
-    do {                                                         \
-        if ((ncols) <= 16)                                       \
-            hipLaunchKernelGGL((KERNEL<16, F_>), __VA_ARGS__);   \
-        else if ((ncols) <= 32)                                  \
-            hipLaunchKernelGGL((KERNEL<32, F_>), __VA_ARGS__);   \
-        else if ((ncols) <= 48)                                  \
-            hipLaunchKernelGGL((KERNEL<48, F_>), __VA_ARGS__);   \
-        else                                                     \
-            hipLaunchKernelGGL((KERNEL<64, F_>), __VA_ARGS__);   \
-    } while (0)
-#define DISPATCH_FMT(fmt, KERNEL, ...)                                                          \
-    do {                                                                                        \
-        switch (fmt) {                                                                          \
-            case SPM_DIA: hipLaunchKernelGGL((KERNEL<SPM_DIA>), __VA_ARGS__); break;            \
-            case SPM_SELL: hipLaunchKernelGGL((KERNEL<SPM_SELL>), __VA_ARGS__); break;          \
-            case SPM_CSR: hipLaunchKernelGGL((KERNEL<SPM_CSR>), __VA_ARGS__); break;            \
-            default: hipLaunchKernelGGL((KERNEL<SPM_ANY>), __VA_ARGS__); break;                 \
-        }                                                                                       \
-    } while (0)
-
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_FMT_MAXC(a.fmt, a.j + 1, k_arn_a1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 0), s, F, a);
+    const size_t lds = lds_bytes(a.j + 1, a.kmax, 0);
+    with_fmt(a.fmt, [&](auto FM) {
+        with_maxc(a.j + 1, [&](auto M) {
+            hipLaunchKernelGGL((k_arn_a1_plain<decltype(M)::value, decltype(FM)::value>), dim3(a.npart, nf),
+                               dim3(TPB), lds, s, F, a);
+        });
+    });
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_FMT_MAXC(a.fmt, a.j, k_arn_a1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 1, a.kmax, 2), s, F, a);
+    const size_t lds = lds_bytes(a.j + 1, a.kmax, 2);
+    with_fmt(a.fmt, [&](auto FM) {
+        with_maxc(a.j, [&](auto M) {
+            hipLaunchKernelGGL((k_arn_a1_fused<decltype(M)::value, decltype(FM)::value>), dim3(a.npart, nf),
+                               dim3(TPB), lds, s, F, a);
+        });
+    });
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_a2, dim3(a.npart, nf), dim3(TPB), lds_bytes(2 * a.j + 4, a.kmax, 1), s, F, a);
+    const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, 1);
+    with_maxc(a.j + 1, [&](auto M) {
+        hipLaunchKernelGGL((k_arn_a2<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
+    });
 }
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_MAXC(a.j + 1, k_arn_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 1), s, F, a);
+    const size_t lds = lds_bytes(a.j + 3, a.kmax, 1);
+    with_maxc(a.j + 1, [&](auto M) {
+        hipLaunchKernelGGL((k_arn_finalize<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
+    });
 }
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_FMT(a.fmt, k_lan_l1_plain, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
+    const size_t lds = lds_bytes(1, a.kmax, 0);
+    with_fmt(a.fmt, [&](auto FM) {
+        hipLaunchKernelGGL((k_lan_l1_plain<decltype(FM)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
+    });
 }
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    DISPATCH_FMT(a.fmt, k_lan_l1_fused, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
+    const size_t lds = lds_bytes(a.j + 3, a.kmax, 0);
+    with_fmt(a.fmt, [&](auto FM) {
+        hipLaunchKernelGGL((k_lan_l1_fused<decltype(FM)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
+    });
 }
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
