@@ -279,7 +279,9 @@ static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<i
     const int64_t nd = (int64_t)seen.size();
     if (nd == 0 || (int64_t)ci.size() * 4 < nd * n * 3) return;
     dld = (n + 255) / 256 * 256;
-    dv.assign((size_t)nd * dld, 0.0);
+    // the device keeps at least 4 diagonal rows (zero rows, offset 0): the <= 4-diagonal
+    // SpMV issues all its loads unconditionally
+    dv.assign((size_t)std::max<int64_t>(nd, 4) * dld, 0.0);
     for (int64_t r = 0; r < n; ++r)
         for (int p = rp[r]; p < rp[r + 1]; ++p) {
             const int o = ci[p] - (int)r;
@@ -288,6 +290,7 @@ static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<i
         }
     offs = seen;
 }
+static int dia_rows(int ndiag) { return ndiag < 4 ? 4 : ndiag; }
 
 // SELL-256 (sliced ELL, slice = 256-row tile) for matrices that are not banded, when the
 // padding stays within 2x nnz; TKHIP_FORCE_CSR=1 disables it.
@@ -348,6 +351,7 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
     if (e == hipSuccess && A->nnz) e = hipMemcpy(A->val, v.data(), A->nnz * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess && !offs.empty()) {
         A->ndiag = (int)offs.size();
+        offs.resize(dia_rows(A->ndiag), 0);
         e = hipMalloc(&A->doff, offs.size() * sizeof(int));
         if (e == hipSuccess) e = hipMalloc(&A->dval, dv.size() * sizeof(double));
         if (e == hipSuccess) e = hipMemcpy(A->doff, offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice);
@@ -574,15 +578,15 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.RED1, (size_t)dc->nvmax * sizeof(double));
         DA(d.RED2, (size_t)dc->nvmax * sizeof(double));
         DA(d.sc, SC_COUNT * sizeof(double));
-        DA(d.h2, KP * sizeof(double));
-        DA(d.g, KP * sizeof(double));
+        DA(d.h2, (KP + 16) * sizeof(double));   // + COEF_TAIL (tk_kernels.hip)
+        DA(d.g, (KP + 16) * sizeof(double));
         DA(d.H, (size_t)KP * KC * sizeof(double));
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
     }
     {
-        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? 1 : (A->sell ? 2 : 3); };
+        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? 1 : 4) : (A->sell ? 2 : 3); };
         dc->fmt = fmt_of(mats[0]);
         for (int f = 1; f < nf; ++f)
             if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;

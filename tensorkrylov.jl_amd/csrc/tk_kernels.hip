@@ -43,13 +43,23 @@ namespace tk {
 // allow; these limits are the largest that compile without spills.
 #define OCC_WAVES(L4, L3) (MAXC <= (L4) ? 4 : (MAXC <= (L3) ? 3 : 2))
 // SpMV-fused kernels: the gather formats need more registers
-#define A1_L4(F) ((F) == 1 || (F) == 3 ? 40 : ((F) == 2 ? 24 : 16))
-#define A1_L3(F) ((F) == 1 || (F) == 3 ? 56 : ((F) == 2 ? 40 : 32))
+#define A1_L4(F) ((F) == 1 || (F) == 3 || (F) == 4 ? 40 : ((F) == 2 ? 24 : 16))
+#define A1_L3(F) ((F) == 1 || (F) == 3 || (F) == 4 ? 56 : ((F) == 2 ? 40 : 32))
 #define OCC_ATTR(L4, L3) __attribute__((amdgpu_waves_per_eu(OCC_WAVES(L4, L3), OCC_WAVES(L4, L3))))
+#ifndef TK_A1_SCALAR
+#define TK_A1_SCALAR 1
+#endif
+#ifndef TK_A2_SCALAR
+#define TK_A2_SCALAR 0
+#endif
+#define COEF_TAIL 16     // h2/g hold kmax+2+COEF_TAIL doubles: register rows may read past kmax+1
 #define COEF_PAD(kmax) ((kmax) + 2 > 64 ? (kmax) + 2 : 64)   // LDS coefficient array length
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 #define GP(T, p) ((__attribute__((address_space(1))) T*)(p))
+// constant address space: wave-uniform reads of data no kernel writes while it runs
+// (coefficient vectors produced by the previous launch) compile to scalar loads
+#define CP4(p) ((const __attribute__((address_space(4))) double*)(p))
 
 // ------------------------------------------------------------------ primitives
 
@@ -143,15 +153,17 @@ __device__ __forceinline__ void st_pair(double* V, int64_t tile_base, int c, int
     GP(d2_t, V + tile_base + vofs(c & ~1, t))[0] = x;
 }
 
-// sum_c V[r,c] * h[c] for c < nc.  h is in LDS (broadcast reads) and zero-padded to
-// MAXC, and R.v[c] is zero for c >= nc (range-checked load): no per-column conditions.
-template <int MAXC>
+// sum_c V[r,c] * h[c] for c < nc.  SCALAR: h is a global coefficient array read with
+// wave-uniform addresses through the constant address space (scalar loads, many in
+// flight); otherwise h is an LDS copy (broadcast reads).  Entries past nc are finite
+// (zeroed at init or earlier coefficients) and meet R.v[c] == 0.
+template <int MAXC, bool SCALAR>
 __device__ __forceinline__ double row_dot(const Row<MAXC>& R, rsrc_t tile, uint32_t toff, int nc,
                                           const double* __restrict__ h) {
     double s = 0.0;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) s += R.v[c] * h[c];
-    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + cofs(c)) * h[c];
+    for (int c = 0; c < MAXC; ++c) s += R.v[c] * (SCALAR ? CP4(h)[c] : h[c]);
+    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + cofs(c)) * (SCALAR ? CP4(h)[c] : h[c]);
     return s;
 }
 
@@ -242,12 +254,35 @@ __device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, 
 // separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
 // FMT: SPM_DIA / SPM_SELL / SPM_CSR fixes the storage at compile time (fewer live
 // registers in the fused kernels); SPM_ANY decides at run time.
-enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3 };
+enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3, SPM_DIAN = 4 };
 template <int FMT, class XF>
 __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
 #pragma clang fp contract(off)
     double s = 0.0;
-    if (FMT == SPM_DIA || (FMT == SPM_ANY && A.ndiag > 0)) {
+    if (FMT == SPM_DIA) {
+        // at most 4 diagonals (the gallery's tridiagonal / convection-diffusion bands); the
+        // device arrays hold at least 4 rows (zero padding, offset 0), so every load is
+        // issued up front from clamped indices and the terms are then summed in order --
+        // one memory round trip instead of one per diagonal.
+        double vv[4], xx[4];
+        bool in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q < 3 || q < A.ndiag) {
+                const int64_t c = r + GP(const int, A.doff)[q];
+                in[q] = q < A.ndiag && c >= 0 && c < A.n;
+                const int64_t cc = c < 0 ? 0 : (c >= A.n ? A.n - 1 : c);
+                vv[q] = ld(A.dval, (int64_t)q * A.dld + r);
+                xx[q] = x(cc);
+            } else {
+                in[q] = false;
+                vv[q] = xx[q] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (in[q]) s = add_rn(s, mul_rn(vv[q], xx[q]));
+    } else if (FMT == SPM_DIAN || (FMT == SPM_ANY && A.ndiag > 0)) {
         for (int q = 0; q < A.ndiag; ++q) {
             const int64_t c = r + GP(const int, A.doff)[q];
             const double v = ld(A.dval, (int64_t)q * A.dld + r);
@@ -347,13 +382,18 @@ template <int MAXC, int FMT>
 __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1_fused(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j;
+    constexpr bool SC = TK_A1_SCALAR;
     const int CP = COEF_PAD(a.kmax);
-    double* h2 = lds;                 // [j], zero-padded
-    double* g = lds + CP;             // [j], zero-padded (g[j] read separately)
-    double* acc = lds + 2 * CP;
-    stage(h2, d.h2, j, CP);
-    stage(g, d.g, j, CP);
-    __syncthreads();
+    const double* h2 = d.h2;
+    const double* g = d.g;            // g[j] read separately
+    double* acc = lds + (SC ? 0 : 2 * CP);
+    if (!SC) {
+        stage(lds, d.h2, j, CP);
+        stage(lds + CP, d.g, j, CP);
+        __syncthreads();
+        h2 = lds;
+        g = lds + CP;
+    }
     const double inv_beta = ld(d.sc, SC_INVBETA);
     const double gj = ld(d.g, j);
     TILE_LOOP
@@ -363,8 +403,8 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
         const double* Ug = d.U;
         const double au = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
         const double up = ld(d.U, r);
-        const double vj = ok ? (up - row_dot(R, tv, toff, j, h2)) * inv_beta : 0.0;
-        const double w = ok ? (au - row_dot(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
+        const double vj = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, j, h2)) * inv_beta : 0.0;
+        const double w = ok ? (au - row_dot<MAXC, SC>(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
         st_pair(d.V, (int64_t)tile * TS, j, threadIdx.x, vj, (j & 1) ? bld(tv, toff + cofs(j - 1)) : 0.0);
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, j, w, tr, acc, 0, first);
@@ -381,11 +421,15 @@ template <int MAXC>
 __global__ __launch_bounds__(TPB) OCC_ATTR(32, 56) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
+    constexpr bool SC = TK_A2_SCALAR;
     const int CP = COEF_PAD(a.kmax);
-    double* h1 = lds;
-    double* acc = lds + CP;
-    stage(h1, d.RED1, nc, CP);
-    __syncthreads();
+    const double* h1 = d.RED1;
+    double* acc = lds + (SC ? 0 : CP);
+    if (!SC) {
+        stage(lds, d.RED1, nc, CP);
+        __syncthreads();
+        h1 = lds;
+    }
     const bool gram = d.track_gram != 0;
     TILE_LOOP
         const rsrc_t tv = mkrsrc(Vt, vrange(nc));
@@ -393,7 +437,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 56) void k_arn_a2(const DFac* __r
         R.load(tv, toff, nc);
         const double vj = bld(tv, toff + cofs(j));
         const double w = ld(d.W, r);
-        const double u = ok ? (w - row_dot(R, tv, toff, nc, h1)) : 0.0;
+        const double u = ok ? (w - row_dot<MAXC, SC>(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
         reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
         const double e[2] = {u * u, vj * ld(d.b, r)};
@@ -409,18 +453,22 @@ template <int MAXC>
 __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
+    constexpr bool SC = TK_A2_SCALAR;
     const int CP = COEF_PAD(a.kmax);
-    double* h2 = lds;
-    double* acc = lds + CP;
-    stage(h2, d.h2, nc, CP);
-    __syncthreads();
+    const double* h2 = d.h2;
+    double* acc = lds + (SC ? 0 : CP);
+    if (!SC) {
+        stage(lds, d.h2, nc, CP);
+        __syncthreads();
+        h2 = lds;
+    }
     const double inv_beta = ld(d.sc, SC_INVBETA);
     TILE_LOOP
         const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
         R.load(tv, toff, nc);
         const double up = ld(d.U, r);
-        const double v = ok ? (up - row_dot(R, tv, toff, nc, h2)) * inv_beta : 0.0;
+        const double v = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, nc, h2)) * inv_beta : 0.0;
         st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? bld(tv, toff + cofs(j)) : 0.0);
         reduce_row<MAXC>(R, tv, toff, nc, v, tr, acc, 0, first);
         const double e[2] = {v * v, v * ld(d.b, r)};
@@ -584,6 +632,13 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         __syncthreads();
     }
     if (kind == POST_INIT_A) {
+        // coefficient arrays start clean (register-row dot products read them past the
+        // current column count, against zero basis entries)
+        for (int i = t; i < kmax + 2 + COEF_TAIL; i += TPB) {
+            st(d.h2, i, 0.0);
+            st(d.g, i, 0.0);
+        }
+        for (int i = t + 1; i < 2 * kmax + 8; i += TPB) st(d.RED2, i, 0.0);
         if (t == 0) {
             const double nrm = sqrt(ld(d.RED1, 0));
             st(d.sc, SC_BNORM, nrm);
@@ -763,9 +818,10 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
 }
 
 // ------------------------------------------------------------------ plain SpMV (test hook)
+template <int FMT>
 __global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ x, double* __restrict__ y) {
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (r < A.n) st(y, r, spmv<SPM_ANY>(A, r, [=](int64_t c) { return ld(x, c); }));
+    if (r < A.n) st(y, r, spmv<FMT>(A, r, [=](int64_t c) { return ld(x, c); }));
 }
 
 // ------------------------------------------------------------------ tile-major gather/scatter
@@ -807,6 +863,7 @@ static void with_fmt(int fmt, F f) {
         case SPM_DIA: f(IC<SPM_DIA>{}); break;
         case SPM_SELL: f(IC<SPM_SELL>{}); break;
         case SPM_CSR: f(IC<SPM_CSR>{}); break;
+        case SPM_DIAN: f(IC<SPM_DIAN>{}); break;
         default: f(IC<SPM_ANY>{}); break;
     }
 }
@@ -827,7 +884,7 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     });
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    const size_t lds = lds_bytes(a.j + 1, a.kmax, 2);
+    const size_t lds = lds_bytes(a.j + 1, a.kmax, TK_A1_SCALAR ? 0 : 2);
     with_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
             hipLaunchKernelGGL((k_arn_a1_fused<decltype(M)::value, decltype(FM)::value>), dim3(a.npart, nf),
@@ -836,13 +893,13 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     });
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, 1);
+    const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_a2<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
 }
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
-    const size_t lds = lds_bytes(a.j + 3, a.kmax, 1);
+    const size_t lds = lds_bytes(a.j + 3, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_finalize<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
@@ -883,7 +940,10 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
 }
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
     const int nb = (int)((A.n + TPB - 1) / TPB);
-    hipLaunchKernelGGL(k_spmv, dim3(nb), dim3(TPB), 0, s, A, x, y);
+    const int fmt = A.ndiag > 0 ? (A.ndiag <= 4 ? SPM_DIA : SPM_DIAN) : (A.sell ? SPM_SELL : SPM_CSR);
+    with_fmt(fmt, [&](auto FM) {
+        hipLaunchKernelGGL((k_spmv<decltype(FM)::value>), dim3(nb), dim3(TPB), 0, s, A, x, y);
+    });
 }
 void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s) {
     const int nb = (int)((n + TPB - 1) / TPB);
