@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--force-comm", action="store_true",
+                    help="1 rank: still build an RCCL communicator and route every step's records "
+                         "through the all-reduce on the exchange stream (the N>1 code path)")
     ap.add_argument("--pmc-mode", action="store_true",
                     help="run exactly one untimed sweep (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -84,6 +87,9 @@ def main():
     if world > 1:
         uid_path = exchange_uid(tkamd, rank)
         ctx.init_comm(uid_path[1], world, rank)
+    elif args.force_comm:
+        ctx.init_comm(tkamd.unique_id(), 1, 0)
+        os.environ["TKHIP_EXCHANGE_ALWAYS"] = "1"
 
     csc = tkamd.assemble_matrix(n, cls)
     nnz = int(csc[0][-1])
@@ -194,7 +200,8 @@ def main():
                                    "step = 1 sweep of K iterations + V*Y (t=%d)"
                                    % (args.config, d, n, cls, method, K, world, t_rank),
                        "d": d, "n_s": n, "nmax": K, "matrix": cls, "method": method,
-                       "parallelism": "factor-partition x%d (RCCL all-reduce of records per iteration)" % world},
+                       "parallelism": "factor-partition x%d (RCCL all-reduce of records per iteration%s)"
+                                      % (world, ", forced on 1 rank" if args.force_comm else "")},
             "roofline": {
                 "bound": "hbm",
                 "kernel": "Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors",

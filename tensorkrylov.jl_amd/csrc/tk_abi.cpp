@@ -68,6 +68,7 @@ struct tk_ctx {
     long cnt[TCLS_N] = {0};
     double* xbuf = nullptr;   // host-allreduce staging
     size_t xcap = 0;
+    std::vector<hipEvent_t> evpool;   // recycled timing events (no hipEventCreate per step)
     // Handles may be destroyed in any order (Julia finalizers, Python GC): matrices and
     // decompositions hold a reference on their context, decompositions on their matrices.
     std::atomic<int> refs{1};
@@ -83,9 +84,17 @@ struct Timer {
         : c(c_), cls(cls_), on(c_->timing >= level), st(s_ ? s_ : c_->stream) {
         if (!on) return;
         hipEvent_t a;
-        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { on = false; return; }
+        if (!take(a) || !take(b)) { on = false; return; }
         hipEventRecord(a, st);
         c->ev[cls].push_back(a);
+    }
+    bool take(hipEvent_t& e) {
+        if (!c->evpool.empty()) {
+            e = c->evpool.back();
+            c->evpool.pop_back();
+            return true;
+        }
+        return hipEventCreate(&e) == hipSuccess;
     }
     ~Timer() {
         if (!on) return;
@@ -105,8 +114,8 @@ static void drain_timers(tk_ctx* c) {
                 c->ms[k] += ms;
                 c->cnt[k] += 1;
             }
-            hipEventDestroy(v[i]);
-            hipEventDestroy(v[i + 1]);
+            c->evpool.push_back(v[i]);
+            c->evpool.push_back(v[i + 1]);
         }
         v.clear();
     }
@@ -145,6 +154,7 @@ static void ctx_release(tk_ctx* c) {
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->xstream);
     drain_timers(c);
+    for (hipEvent_t e : c->evpool) hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->xbuf) hipFree(c->xbuf);
     hipStreamDestroy(c->stream);
@@ -598,7 +608,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
     }
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
-    if (c->comm && c->nranks > 1)
+    // records go through the RCCL exchange whenever factors are spread over ranks;
+    // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
+    const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
+    if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1')))
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
     else
         dc->recv = dc->rec;
@@ -875,7 +888,8 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
 
 tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
     CHECKARG(dc, "NULL decomp");
-    if (dc->method == TK_LANCZOS_REORTH) return fail(TK_ERR_ARG, "tk_decomp_sweep: LanczosReorth needs a host decision per step");
+    // (LanczosReorth steps take their redo decision on the host inside tk_decomp_step,
+    // so its sweep synchronizes once per step; Arnoldi / Lanczos sweeps never wait)
     for (int j = j0; j < j1; ++j) {
         tk_status st = tk_decomp_step(dc, j, nullptr);
         if (st) return st;

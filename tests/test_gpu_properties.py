@@ -240,3 +240,42 @@ def test_tensorkrylov_nonsym_distinct_rhs_vs_oracle(ctx):
     assert conv.niterations == conv_o.niterations
     ref = np.array(conv_o.relative_residual_norm)
     assert np.abs(conv.relative_residual_norm[1:] - ref[1:]).max() <= 1e-10 * ref[1:].max()
+
+
+# ------------------------------------------------------------------ exchange path (N > 1 code)
+@pytest.mark.parametrize("method", [0, 2])
+def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
+    """The multi-rank path -- records summed by ncclAllReduce on the exchange stream, slot
+    events, the receive buffer -- forced on a 1-rank communicator, gives bitwise the same
+    records and basis as the local path (what every rank of an N-GPU run relies on)."""
+    tk = _tk()
+    n, K, d = 3000, 25, 3
+    csc = tk.assemble_matrix(n, "Laplace")
+    rng = np.random.default_rng(5)
+    bs = [_unit(rng.random(n)) for _ in range(d)]
+
+    def run(c):
+        A = tk.DeviceMatrix(c, csc)
+        dev = tk.DeviceDecomposition(c, method, d, 0, [A] * d, bs, K, track_all_gram=True)
+        recs = [dev.init()] + [dev.step(j) for j in range(K)] + [dev.flush()]
+        dev.init(False)                       # asynchronous sweep through the same path
+        dev.sweep(0, K)
+        dev.flush(False)
+        recs2 = dev.records(0, K + 2)
+        V = [dev.basis(f, 0, K + 1) for f in range(d)]
+        dev.close()
+        A.close()
+        return recs, recs2, V
+
+    local = run(ctx)
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    xch = run(c2)
+    c2.close()
+    for a, b in zip(local[0], xch[0]):
+        assert np.array_equal(a, b)
+    for s in range(K + 2):
+        assert np.array_equal(local[1][s], xch[1][s])
+    for a, b in zip(local[2], xch[2]):
+        assert np.array_equal(a, b)
