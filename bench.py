@@ -66,6 +66,10 @@ def main():
     ap.add_argument("--force-comm", action="store_true",
                     help="1 rank: still build an RCCL communicator and route every step's records "
                          "through the all-reduce on the exchange stream (the N>1 code path)")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="diagnostic: on 1 GPU run only rank 0's factor block of an N-rank "
+                         "partition (records exchanged over a 1-rank communicator) to predict "
+                         "the per-GPU step time at N GPUs; the JSON line is marked as emulated")
     ap.add_argument("--pmc-mode", action="store_true",
                     help="run exactly one untimed sweep (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
@@ -83,6 +87,9 @@ def main():
     d, n, cls, method, K, inst = CONFIGS[args.config]
     ctx = tkamd.Context(local_rank)
     part = tkamd.Partition(d, world, rank)
+    if args.emulate_ranks > 1 and world == 1:
+        part = tkamd.Partition(d, args.emulate_ranks, 0)
+        args.force_comm = os.environ.get("TK_EMULATE_NOCOMM") != "1"
     uid_path = None
     if world > 1:
         uid_path = exchange_uid(tkamd, rank)
@@ -114,9 +121,14 @@ def main():
     rng = np.random.default_rng(7)
     Ys = [rng.standard_normal((K, t_rank)) for _ in range(part.nf)]
 
+    host_issue = [0.0, 0]
+
     def sweep():
         dev.init(False)
-        dev.sweep(0, K)
+        h0 = time.perf_counter()
+        dev.sweep(0, K)                 # enqueues K steps; returns before they run
+        host_issue[0] += time.perf_counter() - h0
+        host_issue[1] += 1
         dev.flush(False)
         dev.basis_mul(K, Ys, want=False)
 
@@ -143,6 +155,7 @@ def main():
         sweep()
     barrier()
     elapsed = time.perf_counter() - t0
+    host_us_per_step = 1e6 * host_issue[0] / max(host_issue[1], 1) / K
     step_ms, step_cnt = ctx.timing_read(L.T_STEP)
     vy_ms, vy_cnt = ctx.timing_read(L.T_VY)
     if world > 1:                               # max over ranks (one-hot sum)
@@ -175,13 +188,13 @@ def main():
     if rank == 0:
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
-        if os.path.exists(pmc_path):
+        if os.path.exists(pmc_path) and not args.emulate_ranks:
             try:
                 traffic = json.load(open(pmc_path)).get("hbm_bytes_per_step")
             except Exception:
                 traffic = None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and not args.emulate_ranks:
             cpu = cpu_baseline(csc, n, d, K, args.cpu_seconds)
         out = {
             "metric": "Krylov iterations/sec (d-dim Laplacian tensor Krylov, SpMV+MGS2 per factor)",
@@ -192,6 +205,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True,
+            **({"emulated": "rank 0 of %d on one GPU: per-rank time of an N-GPU run, NOT a "
+                            "whole-job number" % args.emulate_ranks} if args.emulate_ranks else {}),
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
@@ -213,6 +228,7 @@ def main():
                 "algorithmic_bytes_per_launch": alg_step / K,
                 "avg_launch_us": round(step_avg_s * 1e6, 2),
             },
+            "host_issue_us_per_iteration": round(host_us_per_step, 2),
             "basis_mul_mfma": {
                 "avg_us": round(vy_s * 1e6, 2),
                 "GB_s": round(vy_bytes / vy_s / 1e9, 1) if vy_cnt else None,

@@ -559,7 +559,13 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     dc->n = n;
     dc->ld = (n + 255) / 256 * 256;
     dc->ntiles = (int)((n + 255) / 256);
-    dc->npart = std::min(dc->ntiles, 1024);
+    // partial count: a function of n only (bitwise results independent of the factor
+    // partition); TKHIP_NPART overrides it for tuning experiments
+    {
+        const char* e = getenv("TKHIP_NPART");
+        const int cap = e ? std::max(32, atoi(e)) : 1024;
+        dc->npart = std::min(dc->ntiles, cap);
+    }
     dc->nvmax = 2 * kmax + 8;
     dc->mats.assign(mats, mats + nf);
     dc->hf.resize(nf);
@@ -784,11 +790,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         const bool fused = dc->pending;
         if (fused) {
             RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");
-            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         } else {
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");
-            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         }
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, 1, s), "post");

@@ -42,7 +42,7 @@ struct SpM {
 // index it with blockIdx.y, so every launch covers all of this rank's factors.
 struct DFac {
     SpM A;                // A_s
-    double* V;            // basis, tile-major: (r/256)*256*(kmax+1) + c*256 + r%256
+    double* V;            // basis, tile-major, paired columns (tk_kernels.hip header)
     const double* b;      // b_s (n)
     double* W;            // work vector (SpMV output / Lanczos v)
     double* U;            // work vector (w' / Lanczos u)

@@ -241,6 +241,7 @@ __device__ __forceinline__ void store_partials(const double* acc, double* P, int
     for (int c = threadIdx.x; c < nv; c += TPB) GP(double, P)[(int64_t)c * npart + blockIdx.x] = acc[c];
 }
 
+
 // Copy nc coefficients from global to LDS, zero-padded to `pad` entries (caller syncs).
 __device__ __forceinline__ void stage(double* dst, const double* src, int nc, int pad) {
     const int m = nc > pad ? nc : pad;
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 __device__ __forceinline__ void put_gram(double* rec, int kmax, int c, const double* row, double bt,
                                          int tracked) {
     if (tracked)
-        for (int i = threadIdx.x; i <= c; i += TPB) st(rec, rec_gram(kmax) + i, ld(row, i));
+        for (int i = threadIdx.x; i <= c; i += TPB) st(rec, rec_gram(kmax) + i, row[i]);   // row: LDS or global
     if (threadIdx.x == 0) {
         st(rec, rec_bt(kmax), bt);
         st(rec, rec_col(kmax), (double)c);
@@ -618,13 +619,72 @@ __device__ __forceinline__ void put_gram(double* rec, int kmax, int c, const dou
 }
 
 #define POST_LDS_MAX 8192   // doubles of dynamic LDS for Hbar in k_post (kmax <= 88)
+// Arnoldi post-processing of step j (one 256-thread block per factor): from
+// red1 = [h1 (j+1)] (global) and red2 = [h2 (j+1) | |w'|^2 | bt_j | gram_j (j+1)] (LDS or
+// global) write H[:, j] = h1 + h2 and beta = sqrt(|w'|^2 - |h2|^2) (the CGS2 form of
+// src/orthogonal_bases.jl:22-36), g = Hbar h2 for the next step's lazy column, the
+// step's record and scalars.  Hs: LDS for Hbar ((j+1)*(j+2) doubles) or null (global reads).
+__device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const double* red1, const double* red2,
+                         double* Hs, double* h2s, double* sh) {
+    const int j = a.j, kmax = a.kmax, KP = kmax + 2;
+    const int t = threadIdx.x;
+    double* Hc = d.H + (int64_t)j * KP;
+    const int J2 = j + 2;
+    double hh = 0.0;
+    for (int i = t; i <= j; i += TPB) {
+        const double h2 = red2[i];
+        const double hv = ld(red1, i) + h2;
+        st(Hc, i, hv);
+        st(d.h2, i, h2);
+        st(rec, i, hv);
+        h2s[i] = h2;
+        if (Hs) Hs[j * J2 + i] = hv;
+        hh += h2 * h2;
+    }
+    if (Hs)
+        for (int idx = t; idx < j * J2; idx += TPB) {
+            const int i = idx / J2, l = idx - i * J2;
+            Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+        }
+    hh = row16_sum(hh);
+    hh += __shfl_xor(hh, 16);
+    hh += __shfl_xor(hh, 32);
+    if ((t & 63) == 0) sh[t >> 6] = hh;
+    __syncthreads();
+    if (t == 0) {
+        const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+        const double bsq = red2[j + 1] - s2;
+        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+        st(Hc, j + 1, beta);
+        if (Hs) Hs[j * J2 + j + 1] = beta;
+        st(rec, j + 1, beta);
+        st(rec, rec_beta(kmax), beta);
+        st(d.sc, SC_BETA, beta);
+        st(d.sc, SC_INVBETA, 1.0 / beta);
+        st(d.sc, SC_BETAPREV, beta);
+        sh[8] = beta;
+    }
+    __syncthreads();
+    // g = Hbar[0..j+1, 0..j] * h2 (column i of Hbar has rows 0..i+1)
+    for (int l = t; l <= j + 1; l += TPB) {
+        double s = 0.0;
+        for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) {
+            const double hv = Hs ? Hs[i * J2 + l]
+                                 : (i == j ? (l == j + 1 ? sh[8] : ld(Hc, l)) : ld(d.H, (int64_t)i * KP + l));
+            s += hv * h2s[i];
+        }
+        st(d.g, l, s);
+    }
+    put_gram(rec, kmax, j, red2 + j + 3, red2[j + 2], d.track_gram);
+}
+
 __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag,
                                               int clear) {
     __shared__ double sh[16];
     __shared__ double h2s[1024 + 8];
     extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
-    const int j = a.j, kmax = a.kmax, KP = kmax + 2;
+    const int j = a.j, kmax = a.kmax;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
     const int t = threadIdx.x;
     if (clear) {
@@ -651,56 +711,8 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         return;
     }
     if (kind == POST_ARN) {
-        // RED1 = [h1 (j+1)];  RED2 = [h2 (j+1) | s | bt_j | gram_j (j+1)]
-        double* Hc = d.H + (int64_t)j * KP;
-        const int J2 = j + 2;
-        double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // Hbar [i][l]
-        double hh = 0.0;
-        for (int i = t; i <= j; i += TPB) {
-            const double h2 = ld(d.RED2, i);
-            const double hv = ld(d.RED1, i) + h2;
-            st(Hc, i, hv);
-            st(d.h2, i, h2);
-            st(rec, i, hv);
-            h2s[i] = h2;
-            if (Hs) Hs[j * J2 + i] = hv;
-            hh += h2 * h2;
-        }
-        if (Hs)
-            for (int idx = t; idx < j * J2; idx += TPB) {
-                const int i = idx / J2, l = idx - i * J2;
-                Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
-            }
-        hh = row16_sum(hh);
-        hh += __shfl_xor(hh, 16);
-        hh += __shfl_xor(hh, 32);
-        if ((t & 63) == 0) sh[t >> 6] = hh;
-        __syncthreads();
-        if (t == 0) {
-            const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-            const double bsq = ld(d.RED2, j + 1) - s2;
-            const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
-            st(Hc, j + 1, beta);
-            if (Hs) Hs[j * J2 + j + 1] = beta;
-            st(rec, j + 1, beta);
-            st(rec, rec_beta(kmax), beta);
-            st(d.sc, SC_BETA, beta);
-            st(d.sc, SC_INVBETA, 1.0 / beta);
-            st(d.sc, SC_BETAPREV, beta);
-            sh[8] = beta;
-        }
-        __syncthreads();
-        // g = Hbar[0..j+1, 0..j] * h2 (column i of Hbar has rows 0..i+1)
-        for (int l = t; l <= j + 1; l += TPB) {
-            double s = 0.0;
-            for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) {
-                const double hv = Hs ? Hs[i * J2 + l]
-                                     : (i == j ? (l == j + 1 ? sh[8] : ld(Hc, l)) : ld(d.H, (int64_t)i * KP + l));
-                s += hv * h2s[i];
-            }
-            st(d.g, l, s);
-        }
-        put_gram(rec, kmax, j, d.RED2 + j + 3, ld(d.RED2, j + 2), d.track_gram);
+        double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // = launcher's size
+        post_arn(d, a, rec, d.RED1, d.RED2, Hs, h2s, sh);
         return;
     }
     if (kind == POST_ARN_FIN) {
