@@ -227,6 +227,8 @@ struct tk_mat {
     double* dval = nullptr;
     int ndiag = 0;
     int64_t dld = 0;
+    double* dconst = nullptr;
+    int toep = 0;
     long long* sptr = nullptr;
     int* swidth = nullptr;
     int* rowlen = nullptr;
@@ -242,6 +244,8 @@ struct tk_mat {
         m.dval = dval;
         m.ndiag = ndiag;
         m.dld = dld;
+        m.dconst = dconst;
+        m.toep = toep;
         m.sptr = sptr;
         m.swidth = swidth;
         m.rowlen = rowlen;
@@ -259,6 +263,7 @@ static void free_mat(tk_mat* A) {
     hipFree(A->val);
     hipFree(A->doff);
     hipFree(A->dval);
+    hipFree(A->dconst);
     hipFree(A->sptr);
     hipFree(A->swidth);
     hipFree(A->rowlen);
@@ -272,7 +277,8 @@ static void free_mat(tk_mat* A) {
 #define TK_MAX_DIAG 8
 static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<int>& ci,
                       const std::vector<double>& v, std::vector<int>& offs, std::vector<double>& dv,
-                      int64_t& dld) {
+                      int64_t& dld, std::vector<double>& dc, int& toep) {
+    toep = 0;
     offs.clear();
     const char* env = getenv("TKHIP_FORCE_CSR");
     if (env && env[0] == '1') return;
@@ -299,6 +305,24 @@ static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<i
             dv[(size_t)q * dld + r] = v[p];
         }
     offs = seen;
+    // Toeplitz band (the gallery's Laplace / ConvDiff): every in-range position of each
+    // diagonal present with one bit-identical value -> the SpMV reads no matrix values
+    std::vector<int64_t> count(nd, 0);
+    for (int64_t r = 0; r < n; ++r)
+        for (int p = rp[r]; p < rp[r + 1]; ++p)
+            ++count[std::lower_bound(seen.begin(), seen.end(), ci[p] - (int)r) - seen.begin()];
+    dc.assign(std::max<int64_t>(nd, 4), 0.0);
+    bool tz = true;
+    for (int64_t q = 0; q < nd && tz; ++q) {
+        const int64_t o = seen[q];
+        const int64_t r0 = std::max<int64_t>(0, -o), r1 = std::min<int64_t>(n, n - o);
+        if (count[q] != r1 - r0) { tz = false; break; }
+        const double c0 = dv[(size_t)q * dld + r0];
+        for (int64_t r = r0; r < r1; ++r)
+            if (memcmp(&dv[(size_t)q * dld + r], &c0, sizeof(double)) != 0) { tz = false; break; }
+        dc[q] = c0;
+    }
+    toep = tz ? 1 : 0;
 }
 static int dia_rows(int ndiag) { return ndiag < 4 ? 4 : ndiag; }
 
@@ -351,7 +375,8 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
     A->nnz = (int64_t)ci.size();
     std::vector<int> offs;
     std::vector<double> dv;
-    build_dia(n, rp, ci, v, offs, dv, A->dld);
+    std::vector<double> dcv;
+    build_dia(n, rp, ci, v, offs, dv, A->dld, dcv, A->toep);
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipMalloc(&A->rowptr, (n + 1) * sizeof(int));
     if (e == hipSuccess) e = hipMalloc(&A->col, std::max<int64_t>(A->nnz, 1) * sizeof(int));
@@ -366,6 +391,8 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
         if (e == hipSuccess) e = hipMalloc(&A->dval, dv.size() * sizeof(double));
         if (e == hipSuccess) e = hipMemcpy(A->doff, offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice);
         if (e == hipSuccess) e = hipMemcpy(A->dval, dv.data(), dv.size() * sizeof(double), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&A->dconst, dcv.size() * sizeof(double));
+        if (e == hipSuccess) e = hipMemcpy(A->dconst, dcv.data(), dcv.size() * sizeof(double), hipMemcpyHostToDevice);
     }
     if (e == hipSuccess && offs.empty()) {
         std::vector<long long> sptr;
@@ -602,7 +629,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.gidx = gi;
     }
     {
-        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? 1 : 4) : (A->sell ? 2 : 3); };
+        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? (A->toep ? 5 : 1) : 4) : (A->sell ? 2 : 3); };
         dc->fmt = fmt_of(mats[0]);
         for (int f = 1; f < nf; ++f)
             if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;

@@ -28,6 +28,8 @@ struct SpM {
     const double* dval;   // DIA values [ndiag][dld]: dval[q*dld + r] = A[r, r + doff[q]]
     int ndiag;            // > 0: DIA is used
     int64_t dld;
+    const double* dconst; // Toeplitz band: the one value of each diagonal (>= 4 entries)
+    int toep;             // 1: every diagonal is constant and complete (dconst valid)
     // SELL-256: slice = one 256-row tile; entry q of row r at sptr[r/256] + q*256 + r%256
     const long long* sptr;  // (ntiles) slot offset of each slice
     const int* swidth;    // (ntiles) slice width = max row length in the slice

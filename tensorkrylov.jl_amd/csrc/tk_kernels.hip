@@ -43,8 +43,8 @@ namespace tk {
 // allow; these limits are the largest that compile without spills.
 #define OCC_WAVES(L4, L3) (MAXC <= (L4) ? 4 : (MAXC <= (L3) ? 3 : 2))
 // SpMV-fused kernels: the gather formats need more registers
-#define A1_L4(F) ((F) == 1 || (F) == 3 || (F) == 4 ? 40 : ((F) == 2 ? 24 : 16))
-#define A1_L3(F) ((F) == 1 || (F) == 3 || (F) == 4 ? 56 : ((F) == 2 ? 40 : 32))
+#define A1_L4(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 40 : ((F) == 2 ? 24 : 16))
+#define A1_L3(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 56 : ((F) == 2 ? 40 : 32))
 #define OCC_ATTR(L4, L3) __attribute__((amdgpu_waves_per_eu(OCC_WAVES(L4, L3), OCC_WAVES(L4, L3))))
 #ifndef TK_A1_SCALAR
 #define TK_A1_SCALAR 1
@@ -255,12 +255,12 @@ __device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, 
 // separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
 // FMT: SPM_DIA / SPM_SELL / SPM_CSR fixes the storage at compile time (fewer live
 // registers in the fused kernels); SPM_ANY decides at run time.
-enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3, SPM_DIAN = 4 };
+enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3, SPM_DIAN = 4, SPM_DIAT = 5 };
 template <int FMT, class XF>
 __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
 #pragma clang fp contract(off)
     double s = 0.0;
-    if (FMT == SPM_DIA) {
+    if (FMT == SPM_DIA || FMT == SPM_DIAT) {
         // at most 4 diagonals (the gallery's tridiagonal / convection-diffusion bands); the
         // device arrays hold at least 4 rows (zero padding, offset 0), so every load is
         // issued up front from clamped indices and the terms are then summed in order --
@@ -273,7 +273,7 @@ __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
                 const int64_t c = r + GP(const int, A.doff)[q];
                 in[q] = q < A.ndiag && c >= 0 && c < A.n;
                 const int64_t cc = c < 0 ? 0 : (c >= A.n ? A.n - 1 : c);
-                vv[q] = ld(A.dval, (int64_t)q * A.dld + r);
+                vv[q] = FMT == SPM_DIAT ? CP4(A.dconst)[q] : ld(A.dval, (int64_t)q * A.dld + r);
                 xx[q] = x(cc);
             } else {
                 in[q] = false;
@@ -876,6 +876,7 @@ static void with_fmt(int fmt, F f) {
         case SPM_SELL: f(IC<SPM_SELL>{}); break;
         case SPM_CSR: f(IC<SPM_CSR>{}); break;
         case SPM_DIAN: f(IC<SPM_DIAN>{}); break;
+        case SPM_DIAT: f(IC<SPM_DIAT>{}); break;
         default: f(IC<SPM_ANY>{}); break;
     }
 }
@@ -952,7 +953,7 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
 }
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
     const int nb = (int)((A.n + TPB - 1) / TPB);
-    const int fmt = A.ndiag > 0 ? (A.ndiag <= 4 ? SPM_DIA : SPM_DIAN) : (A.sell ? SPM_SELL : SPM_CSR);
+    const int fmt = A.ndiag > 0 ? (A.ndiag <= 4 ? (A.toep ? SPM_DIAT : SPM_DIA) : SPM_DIAN) : (A.sell ? SPM_SELL : SPM_CSR);
     with_fmt(fmt, [&](auto FM) {
         hipLaunchKernelGGL((k_spmv<decltype(FM)::value>), dim3(nb), dim3(TPB), 0, s, A, x, y);
     });

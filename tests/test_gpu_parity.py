@@ -59,6 +59,30 @@ def test_spmv_bit_exact(ctx, cls, n, force_csr, monkeypatch):
     A.close()
 
 
+@pytest.mark.parametrize("n,offs", [(1000, (-1, 0, 1)), (777, (-2, 0, 3)), (600, (-1, 0, 1, 2)),
+                                    (500, (-3, -1, 0, 1, 4, 5))])
+def test_spmv_general_band_bit_exact(ctx, n, offs):
+    """Banded matrices with varying diagonal values (DIA, not Toeplitz; 6 diagonals: the
+    runtime-loop DIA) and a Toeplitz band with one entry perturbed (must not take the
+    constant-diagonal path)."""
+    tk = _tk()
+    rng = np.random.default_rng(n)
+    A = np.zeros((n, n))
+    for o in offs:
+        idx = np.arange(max(0, -o), min(n, n - o))
+        A[idx, idx + o] = rng.standard_normal(len(idx))
+    for M in (A, O.laplace_dense(n)):
+        if M is not A:
+            M = M.copy()
+            M[n // 2, n // 2] *= 1.0 + 1e-15      # breaks the Toeplitz structure by 1 ulp
+        csc = O.dense_to_csc(M)
+        D = tk.DeviceMatrix(ctx, csc)
+        assert D.format > 0
+        x = rng.standard_normal(n)
+        assert np.array_equal(D.matvec(x), O.csc_matvec_fast(csc, x))
+        D.close()
+
+
 def test_spmv_one_based_julia_csc(ctx):
     """Julia hands over 1-based Int64 colptr/rowval unchanged."""
     tk = _tk()
@@ -117,6 +141,26 @@ def test_arnoldi_matches_oracle(ctx, cls, n, K):
         assert np.abs(bt[1:] - bt_ref[1:]).max() <= 1e-14
         Gref = np.tril(fo.V[:, :K + 1].T @ fo.V[:, :K + 1])
         assert np.abs(np.tril(G) - Gref).max() <= 1e-13
+
+
+def test_arnoldi_general_band_matches_oracle(ctx):
+    """Arnoldi over a non-Toeplitz band (the DIA path that streams matrix values)."""
+    tk = _tk()
+    n, K = 900, 30
+    rng = np.random.default_rng(9)
+    A = np.diag(4.0 + rng.random(n)) + np.diag(-rng.random(n - 1), 1) + np.diag(-rng.random(n - 1), -1)
+    csc = O.dense_to_csc(A)
+    bs = _rhs(n, 2, 4, distinct=True)
+    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K)
+    for f, b in enumerate(bs):
+        fo = O.Factor(csc, b, K)
+        for j in range(1, K + 1):
+            fo.arnoldi_mgs(j)
+        Hd = np.zeros((K + 1, K))
+        for j in range(K):
+            Hd[:j + 2, j] = recs[j + 1][f, :j + 2]
+        assert np.abs(Hd - fo.H[:K + 1, :K]).max() <= 1e-12 * np.abs(fo.H).max()
+        assert np.abs(V[f] - fo.V[:, :K + 1]).max() <= 1e-12
 
 
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20)])
