@@ -232,17 +232,18 @@ def test_lanczos_reorth_matches_oracle(ctx):
 
 
 # ------------------------------------------------------------------ driver vs golden / oracle
-def test_tensorkrylov_laplace_golden(ctx):
-    """Recorded reference trajectory (experiments/data/reproduction_data/laplace_new,
-    d=5, TensorLanczosReorth) through the product driver on the GPU."""
+@pytest.mark.parametrize("d", [5, 10])
+def test_tensorkrylov_laplace_golden(ctx, d):
+    """Recorded reference trajectories (experiments/data/reproduction_data/laplace_new,
+    d=5 and d=10, TensorLanczosReorth) through the product driver on the GPU."""
     tk = _tk()
     g = json.load(open(os.path.join(HERE, "golden", "reproduction.json")))["laplace_new"]
-    d, n, K = 5, 200, 51
-    b = np.array(g["rhs"]["5"])
+    n, K = 200, 51
+    b = np.array(g["rhs"][str(d)])
     A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
     conv = tk.ConvergenceData(K)
     tk.tensorkrylov(conv, A, [b.copy() for _ in range(d)], 1e-9, K, "TensorLanczosReorth", ctx=ctx)
-    ref = np.array(g["convergence"]["5"]["relative_residual_norm"][:K])
+    ref = np.array(g["convergence"][str(d)]["relative_residual_norm"][:K])
     rel = np.abs(conv.relative_residual_norm[1:] - ref[1:]) / ref[1:]
     assert rel.max() <= 1e-10
 
