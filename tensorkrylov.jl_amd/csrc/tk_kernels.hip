@@ -132,17 +132,23 @@ __device__ __forceinline__ void chunk_reduce(const double (&x)[CH], double* __re
 
 // Row of V held in VGPRs: v[c] = V[r, c] for c < MAXC, zero for c >= nc (pairs beyond
 // the resource's range read as zero; the odd half of the last pair is cleared here).
+// `last` = V[r, nc-1], the newest column, picked while loading (a second load of it would
+// miss the cache: V loads are non-temporal).
 template <int MAXC>
 struct Row {
     static_assert(MAXC % 2 == 0, "register rows hold whole column pairs");
     double v[MAXC];
+    double last;
     __device__ __forceinline__ void load(rsrc_t tile, uint32_t toff, int nc) {
+        last = 0.0;
 #pragma unroll
         for (int p = 0; p < MAXC / 2; ++p) {
             const d2_t x = bld2(tile, toff + (uint32_t)p * (TPB * 16));
             v[2 * p] = x.x;
             v[2 * p + 1] = 2 * p + 1 < nc ? x.y : 0.0;
+            last = 2 * p == nc - 1 ? x.x : (2 * p + 1 == nc - 1 ? x.y : last);
         }
+        if (nc > MAXC) last = bld(tile, toff + cofs(nc - 1));
     }
 };
 
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double w = ok ? (au - row_dot<MAXC, SC>(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
-        st_pair(d.V, (int64_t)tile * TS, j, threadIdx.x, vj, (j & 1) ? bld(tv, toff + cofs(j - 1)) : 0.0);
+        st_pair(d.V, (int64_t)tile * TS, j, threadIdx.x, vj, (j & 1) ? R.last : 0.0);
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, j, w, tr, acc, 0, first);
         const double e1[1] = {vj * w};
@@ -419,7 +425,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
 // (both need only V[r, 0..j], already in registers):
 //   P2 = [ <V[:,c],U> (c<=j), <U,U>, <v_j,b> | gram <V[:,c],v_j> (c<=j) ]
 template <int MAXC>
-__global__ __launch_bounds__(TPB) OCC_ATTR(32, 56) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2(const DFac* __restrict__ F, KArgs a) {
     KERNEL_PROLOGUE
     const int j = a.j, nc = j + 1;
     constexpr bool SC = TK_A2_SCALAR;
@@ -436,7 +442,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 56) void k_arn_a2(const DFac* __r
         const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
         R.load(tv, toff, nc);
-        const double vj = bld(tv, toff + cofs(j));
+        const double vj = R.last;
         const double w = ld(d.W, r);
         const double u = ok ? (w - row_dot<MAXC, SC>(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
         R.load(tv, toff, nc);
         const double up = ld(d.U, r);
         const double v = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, nc, h2)) * inv_beta : 0.0;
-        st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? bld(tv, toff + cofs(j)) : 0.0);
+        st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? R.last : 0.0);
         reduce_row<MAXC>(R, tv, toff, nc, v, tr, acc, 0, first);
         const double e[2] = {v * v, v * ld(d.b, r)};
         reduce_scalars<2>(e, tr, acc, nc, first);
