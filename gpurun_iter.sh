@@ -9,5 +9,5 @@ cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --st
 echo "prof EXIT $?"
 cd $R; tail -2 gpurun_out/t_gpu.log
 for C in C2_xch C2 C1 C3 C4; do python3 -c "
-import json; d=json.loads(open('gpurun_out/bench_$C.log').read().strip().split('\n')[-1]); print('$C', d['value'], d['roofline']['achieved'], d['roofline']['frac'], {k:v['avg_us'] for k,v in d['kernels'].items()})"; done
+import json; d=json.loads(open('gpurun_out/bench_$C.log').read().strip().split('\n')[-1]); print('$C', d['value'], d['roofline']['achieved'], d['roofline']['frac'], {k:v['avg_us'] for k,v in d['kernels'].items()}, 'e2e', (d.get('end_to_end') or {}).get('iterations_s'))"; done
 head -14 gpurun_out/prof_c2/run_kernel_stats.csv | cut -d, -f1-4

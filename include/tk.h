@@ -44,7 +44,8 @@ enum {
     TK_ERR_ALLOC = 3,    /* device or host allocation failed                  */
     TK_ERR_STATE = 4,    /* call out of sequence (e.g. step j != next step)   */
     TK_ERR_RCCL = 5,     /* RCCL error                                         */
-    TK_ERR_NODEV = 6     /* no usable gfx950 device                            */
+    TK_ERR_NODEV = 6,    /* no usable gfx950 device                            */
+    TK_BREAKDOWN = 7     /* compressed norm breakdown (src/utils.jl:7-14, :395)  */
 };
 
 /* Orthonormalization types: src/decompositions.jl:120-176 (TensorArnoldi,
@@ -171,6 +172,26 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
  * 1 = the dominant streaming kernel (Arnoldi/Lanczos projection), 2 = basis_mul. */
 tk_status tk_timing_enable(tk_ctx* ctx, int on);
 tk_status tk_timing_read(tk_ctx* ctx, int cls, double* total_ms, long* launches);
+
+/* ---------------------------------------------------------------- compressed side (host)
+ * The k-sized per-iteration work of tensorkrylov! (no GPU needed).
+ * Matrices are column-major; factor s's k x k block starts at s*k*k, its b~ at s*k, its
+ * k x t Y_s at s*k*t. */
+
+/* solve_compressed_system (src/tensor_krylov_method.jl:10-34, src/utils.jl:501-523):
+ * lambda[j] = omega[j] / lmin and Y_s[:, j] = exp(-alpha[j]/lmin * first(H)) b~_s, where
+ * first(H) = Symmetric(H1, :L) if `symmetric` (one eigendecomposition serves all t terms)
+ * and the full H1 otherwise (Pade scaling-and-squaring exponential per term). */
+tk_status tk_compressed_solve(int d, int k, const double* H1, int symmetric, const double* bt, int t,
+                              const double* alpha, const double* omega, double lmin, double* lambda,
+                              double* Y);
+
+/* residualnorm! + compressed_residual (src/utils.jl:371-443, Lemma 3.4): H = the d k x k
+ * minors, subdiag[s] = H_s[k+1, k].  Returns TK_BREAKDOWN (with *r_comp set) when the
+ * compressed squared residual is negative, as the reference throws CompressedNormBreakdown. */
+tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* lambda, const double* Y,
+                          const double* subdiag, const double* bt, double bnorm, double* r_comp,
+                          double* r_norm);
 
 #ifdef __cplusplus
 }

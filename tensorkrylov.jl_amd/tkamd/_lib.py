@@ -64,6 +64,8 @@ def lib():
         "tk_decomp_basis_mul": (I, [P, I, I, DP, DP]),
         "tk_timing_enable": (I, [P, I]),
         "tk_timing_read": (I, [P, I, DP, ctypes.POINTER(ctypes.c_long)]),
+        "tk_compressed_solve": (I, [I, I, DP, I, DP, I, DP, DP, ctypes.c_double, DP, DP]),
+        "tk_residualnorm": (I, [I, I, I, DP, DP, DP, DP, DP, ctypes.c_double, DP, DP]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -79,7 +81,10 @@ EXPORTS = ("tk_last_error", "tk_version", "tk_ctx_create", "tk_ctx_destroy", "tk
            "tk_matrix_from_csc", "tk_matrix_from_csr", "tk_matrix_destroy", "tk_matrix_format", "tk_matvec",
            "tk_record_len", "tk_decomp_create", "tk_decomp_destroy", "tk_decomp_init",
            "tk_decomp_step", "tk_decomp_sweep", "tk_decomp_flush", "tk_decomp_records",
-           "tk_decomp_get_basis", "tk_decomp_basis_mul", "tk_timing_enable", "tk_timing_read")
+           "tk_decomp_get_basis", "tk_decomp_basis_mul", "tk_timing_enable", "tk_timing_read",
+           "tk_compressed_solve", "tk_residualnorm")
+
+TK_BREAKDOWN = 7
 
 
 def check(status):

@@ -11,6 +11,7 @@ system (none of it touches n-length data):
     MVnorm / tensorinnerprod               src/utils.jl:132-443 (Lemma 3.4)
 Differences from the reference are performance-only: the coefficient tables are loaded
 once (the reference re-reads the CSV every iteration, src/approximation.jl:162-163);
+the compressed solve and the residual run in native host code (libtkhip, tk_host.cpp):
 exp(gamma_j * Symmetric(H)) for all t terms comes from ONE eigendecomposition
 (exp(gH) = Q exp(g L) Q'); the O(d^3 t^2) masked products become leave-one-out /
 leave-two-out elementwise products.  Exact-arithmetic results are identical.
@@ -164,100 +165,51 @@ class ApproximationData:
 
 
 # ------------------------------------------------------------------ compressed solve
+# Both functions run in libtkhip's host code (csrc/tk_host.cpp); they need no GPU.
 
 def solve_compressed_system(H1, btilde, approx, lmin, symmetric):
     """y = sum_j omega_j/lmin * exp(-alpha_j/lmin * first(H)) btilde_s, as the Kruskal
     tensor (lambda, [Y_s]) of src/tensor_krylov_method.jl:10-34.  first(H) is
-    Symmetric(H_1, :L) for SymInstance (src/tensor_struct.jl:259)."""
-    lam_inv = 1.0 / lmin
-    lam = lam_inv * approx.omega
-    gam = -approx.alpha * lam_inv
-    B = np.stack(btilde, axis=1)                       # k x d
-    if symmetric:
-        L = np.tril(H1)
-        S = L + np.tril(L, -1).T
-        w, Q = np.linalg.eigh(S)
-        C = Q.T @ B                                    # k x d
-        E = np.exp(np.outer(w, gam))                   # k x t
-        Ys = [Q @ (E * C[:, s:s + 1]) for s in range(B.shape[1])]
-    else:
-        import scipy.linalg
-        t = len(gam)
-        Ys = [np.empty((H1.shape[0], t)) for _ in range(B.shape[1])]
-        for j in range(t):
-            Ej = scipy.linalg.expm(gam[j] * H1)
-            P = Ej @ B
-            for s in range(B.shape[1]):
-                Ys[s][:, j] = P[:, s]
-    return lam, Ys
-
-
-# ------------------------------------------------------------------ residual (Lemma 3.4)
-
-def _leave_out(stack):
-    """pre[s] = prod_{q<s}, suf[s] = prod_{q>s} of a (d, t, t) stack (elementwise)."""
-    d = stack.shape[0]
-    one = np.ones_like(stack[0])
-    pre = [one]
-    for s in range(d - 1):
-        pre.append(pre[-1] * stack[s])
-    suf = [one] * d
-    acc = one
-    for s in range(d - 1, -1, -1):
-        suf[s] = acc
-        acc = acc * stack[s]
-    return pre, suf
+    Symmetric(H_1, :L) for SymInstance (src/tensor_struct.jl:259).  -> tk_compressed_solve"""
+    import ctypes
+    from . import _lib as L
+    k = H1.shape[0]
+    d = len(btilde)
+    alpha = np.ascontiguousarray(approx.alpha, dtype=np.float64)
+    omega = np.ascontiguousarray(approx.omega, dtype=np.float64)
+    t = len(alpha)
+    Hc = np.ascontiguousarray(np.asarray(H1, dtype=np.float64).T)        # column-major k x k
+    B = np.ascontiguousarray(np.stack([np.asarray(b, dtype=np.float64)[:k] for b in btilde]))
+    lam = np.empty(t)
+    Y = np.empty((d, t, k))                                              # [s][j][i] = column-major k x t
+    L.check(L.lib().tk_compressed_solve(d, k, L.dptr(Hc), 1 if symmetric else 0, L.dptr(B), t,
+                                        L.dptr(alpha), L.dptr(omega), ctypes.c_double(lmin),
+                                        L.dptr(lam), L.dptr(Y)))
+    return lam, [Y[s].T for s in range(d)]
 
 
 def residualnorm(Hs, lam, Ys, k, subdiag, btilde, b_norm):
     """residualnorm! + compressed_residual (src/utils.jl:371-443).
     Hs: d k x k minors (full), Ys: d k x t, subdiag[s] = H_s[k+1, k].
-    Returns (r_comp, r_norm); raises CompressedNormBreakdown when r_comp < 0."""
+    Returns (r_comp, r_norm); raises CompressedNormBreakdown when r_comp < 0.
+    -> tk_residualnorm"""
+    import ctypes
+    from . import _lib as L
     d = len(Ys)
     t = len(lam)
-    Y = np.stack(Ys)                                   # d x k x t
-    Ly = np.tril(np.einsum("ski,skj->sij", Y, Y))      # lower(Y_s' Y_s)
-    Lam = np.tril(np.outer(lam, lam))
-    W = np.tril(np.full((t, t), 2.0), -1) + np.eye(t)  # weights: 1 on diag, 2 below
-    pre, suf = _leave_out(Ly)
-    loo = [pre[s] * suf[s] for s in range(d)]          # prod_{q != s} Ly_q
-    # first term: sum_s beta_s^2 * squared_tensor_entries(Ly[-s], Gamma_s)
-    res = 0.0
-    for s in range(d):
-        yk = Y[s, k - 1, :]
-        Gam = np.tril(np.outer(yk, yk)) * Lam
-        res += subdiag[s] ** 2 * float(np.sum(W * Gam * loo[s]))
-    # compressed residual
-    Z = np.einsum("sab,sbt->sat", np.stack(Hs), Y)     # Z_s = H_s Y_s
-    X = np.einsum("ski,skj->sij", Y, Z)                # X_s = Y_s' Z_s
-    Lz = np.tril(np.einsum("ski,skj->sij", Z, Z))
-    term = np.zeros((t, t))
-    for s in range(d):
-        term += loo[s] * Lz[s]
-    for s in range(d):
-        for r in range(d):
-            if r == s:
-                continue
-            a, b = (s, r) if s < r else (r, s)
-            mid = np.ones((t, t))
-            for q in range(a + 1, b):
-                mid = mid * Ly[q]
-            term += pre[a] * mid * suf[b] * X[s] * X[r].T
-    hy_norm = float(np.sum(W * Lam * term))
-    F0 = Y[:, 0, :]                                    # first rows  d x t
-    G0 = Z[:, 0, :]
-    fpre = np.ones_like(F0)
-    for s in range(1, d):
-        fpre[s] = fpre[s - 1] * F0[s - 1]
-    fsuf = np.ones_like(F0)
-    for s in range(d - 2, -1, -1):
-        fsuf[s] = fsuf[s + 1] * F0[s + 1]
-    hy_b = float(np.sum(lam[None, :] * G0 * fpre * fsuf)) * b_norm
-    bnorm2 = float(np.prod([np.dot(b, b) for b in btilde]))
-    r_comp = hy_norm - 2 * hy_b + bnorm2
-    if r_comp < 0.0:
-        raise CompressedNormBreakdown(r_comp)
-    return r_comp, math.sqrt(res + r_comp)
+    H = np.ascontiguousarray(np.stack([np.asarray(h, dtype=np.float64)[:k, :k].T for h in Hs]))
+    Y = np.ascontiguousarray(np.stack([np.asarray(y, dtype=np.float64).T for y in Ys]))
+    B = np.ascontiguousarray(np.stack([np.asarray(b, dtype=np.float64)[:k] for b in btilde]))
+    lamc = np.ascontiguousarray(lam, dtype=np.float64)
+    sub = np.ascontiguousarray(subdiag, dtype=np.float64)
+    rc = ctypes.c_double()
+    rn = ctypes.c_double()
+    st = L.lib().tk_residualnorm(d, k, t, L.dptr(H), L.dptr(lamc), L.dptr(Y), L.dptr(sub), L.dptr(B),
+                                 ctypes.c_double(b_norm), ctypes.byref(rc), ctypes.byref(rn))
+    if st == L.TK_BREAKDOWN:
+        raise CompressedNormBreakdown(rc.value)
+    L.check(st)
+    return rc.value, rn.value
 
 
 def orthogonality_loss_from_gram(G, k):

@@ -57,6 +57,7 @@ class TensorDecomposition:
         self.ctx = ctx
         self._backend = backend
         self.dev = None
+        self._issued = {}
 
     # -------------------------------------------------------------- device setup
     def _attach(self, b):
@@ -102,8 +103,25 @@ class TensorDecomposition:
 
     def orthonormalize(self, k):
         """orthonormalize!(td, k) (src/orthogonal_bases.jl:162-180), k 1-based."""
+        self.issue(k)
+        self.collect(k)
+
+    def issue(self, k):
+        """Enqueue step k on the device without waiting (the driver overlaps it with the
+        host's compressed solve of step k-1).  Columns <= k-1 of V, H and b~ are not
+        touched by step k, so results are the same as with orthonormalize(k)."""
         j = k - 1
-        rec = self.dev.step(j)
+        if hasattr(self.dev, "step_async"):
+            self.dev.step_async(j)
+        else:
+            self._issued[j] = self.dev.step(j)
+
+    def collect(self, k):
+        """Records of an issued step k -> the host mirror of H, b~ and the Gram rows."""
+        j = k - 1
+        rec = self._issued.pop(j, None)
+        if rec is None:
+            rec = self.dev.records(j + 1, j + 2)[0]
         self._apply_step(j, rec)
         self._apply_gram(rec)
 

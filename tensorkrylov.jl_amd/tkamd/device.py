@@ -138,6 +138,10 @@ class DeviceDecomposition:
         L.check(self.ctx._lib.tk_decomp_step(self.h, int(j), L.dptr(r)))
         return r
 
+    def step_async(self, j):
+        """Enqueue step j; its record stays on the device (records(j+1, j+2))."""
+        L.check(self.ctx._lib.tk_decomp_step(self.h, int(j), None))
+
     def sweep(self, j0, j1):
         L.check(self.ctx._lib.tk_decomp_sweep(self.h, int(j0), int(j1)))
 

@@ -7,6 +7,8 @@ ranks every rank runs this same loop; the device all-reduces each step's per-fac
 records so the k-sized compressed solve below is evaluated redundantly and
 identically on every rank.
 """
+import time
+
 import numpy as np
 
 from .compressed import (ApproximationData, CompressedNormBreakdown, SpectralData,
@@ -16,10 +18,16 @@ from .structures import ConvergenceData, KruskalTensor, kronprodnorm
 
 
 def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbose=False,
-                 backend=None, keep_decomposition=False):
+                 backend=None, keep_decomposition=False, pipelined=True):
     """tensorkrylov!(convergence_data, A, b, tol, nmax, orthonormalization_type).
     Returns the approximate solution as a KruskalTensor of the LOCAL factors
-    (x_s = V_s y_s) on convergence, else None."""
+    (x_s = V_s y_s) on convergence, else None.
+
+    pipelined: step k+1 is enqueued on the device before the host evaluates iteration k
+    (compressed solve, residual), so device and host work overlap.  Step k+1 leaves
+    V[:, 1:k], H[1:k, 1:k] and b~[1:k] untouched, so every iterate, residual and the
+    returned solution are those of the sequential loop; on convergence at k the extra
+    step's result is simply never read."""
     if isinstance(method, str):
         method = METHODS[method]
     d = len(A)
@@ -27,12 +35,23 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
     td = method(A, nmax, ctx=ctx, partition=partition, backend=backend)   # :51
     symmetric = A.symmetric
     x = None
+    t_start = time.perf_counter()
+    conv.timing = {}
     try:
         td.orthonormalize_first(b)                                  # :53 (+ b~ init, :55)
+        t_loop = time.perf_counter()
+        conv.timing["setup_s"] = t_loop - t_start                   # upload A_s, b_s; step 1
         spectral = SpectralData(A, nmax)                            # :57
         approx = ApproximationData(tol, symmetric)                  # :58
+        if pipelined and nmax >= 2:
+            td.issue(2)
         for k in range(2, nmax + 1):                                # :63
-            td.orthonormalize(k)                                    # :66
+            if pipelined:
+                td.collect(k)                                       # :66
+                if k + 1 <= nmax:
+                    td.issue(k + 1)                                 # overlaps the host work below
+            else:
+                td.orthonormalize(k)                                # :66
             Hm = td.minors(k)                                       # :68
             bm = [td.btilde[s, :k].copy() for s in range(d)]        # update_rhs! :71
             spectral.update(d)                                      # :72
@@ -47,6 +66,7 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
                     print("Early termination at k = %d due to compressed norm breakdown" % k)
                 conv.niterations = k - 1
                 conv.resize(k - 1)
+                conv.timing["loop_s"] = time.perf_counter() - t_loop
                 return None
             rel = r_norm / b_norm                                   # :99
             conv.relative_residual_norm[k - 1] = rel
@@ -59,9 +79,11 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
                 X = td.dev.basis_mul(k, [Ys[s] for s in loc])
                 x = KruskalTensor(lam.copy(), X)
                 x.factors = loc
+                conv.timing["loop_s"] = time.perf_counter() - t_loop
                 if verbose:
                     print("Convergence")
                 return x
+        conv.timing["loop_s"] = time.perf_counter() - t_loop
         if verbose:
             print("No convergence")
         return None

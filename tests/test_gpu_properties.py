@@ -281,3 +281,28 @@ def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
         assert np.array_equal(local[1][s], xch[1][s])
     for a, b in zip(local[2], xch[2]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("method", ["TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"])
+def test_pipelined_driver_identical_to_sequential(ctx, method):
+    """The driver enqueues step k+1 before the host evaluates iteration k; every iterate,
+    residual and the returned solution must be those of the sequential loop (bitwise)."""
+    tk = _tk()
+    d, n, K = 4, 3000, 30
+    rng = np.random.default_rng(21)
+    b = [_unit(rng.random(n)) for _ in range(d)]
+    A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
+    out = []
+    for pipe in (False, True):
+        conv = tk.ConvergenceData(K)
+        x = tk.tensorkrylov(conv, A, [v.copy() for v in b], 1e-6, K, method, ctx=ctx, pipelined=pipe)
+        out.append((conv, x))
+    (c0, x0), (c1, x1) = out
+    assert c0.niterations == c1.niterations
+    assert np.array_equal(c0.relative_residual_norm, c1.relative_residual_norm)
+    assert np.array_equal(c0.orthogonality_data, c1.orthogonality_data)
+    assert (x0 is None) == (x1 is None)
+    if x0 is not None:
+        assert np.array_equal(x0.lam, x1.lam)
+        for a_, b_ in zip(x0.fmat, x1.fmat):
+            assert np.array_equal(a_, b_)
