@@ -264,3 +264,73 @@ def test_handles_destroyed_in_any_order_without_gpu():
     assert lib.tk_decomp_destroy(None) == 0
     assert lib.tk_matrix_destroy(None) == 0
     assert lib.tk_ctx_destroy(None) == 0
+
+
+# ------------------------------------------------------------------ native compressed side edge cases
+@pytest.mark.parametrize("k", [1, 2, 5, 60, 150])
+@pytest.mark.parametrize("scale", [1e-4, 0.3, 3.0, 40.0])
+def test_native_compressed_solve_sym_and_nonsym(k, scale):
+    """tk_compressed_solve vs eigh / scipy expm across sizes and norms that select every
+    Pade degree (3, 5, 7, 9, 13) and the scaling-and-squaring branch."""
+    import scipy.linalg
+    rng = np.random.default_rng(k)
+    d, t = 3, 4
+    M = rng.standard_normal((k, k))
+    M /= np.linalg.norm(M, 1)                     # ||g H||_1 <= 2 * scale: degree set by scale
+    bt = [rng.standard_normal(k) for _ in range(d)]
+
+    class Ap:
+        alpha = np.linspace(0.1, 2.0, t)
+        omega = np.linspace(1.0, 0.2, t)
+    lmin = 1.0 / scale
+    for sym in (True, False):
+        H = (M + M.T) / 2 if sym else M
+        lam, Ys = tkamd.solve_compressed_system(H, bt, Ap, lmin, sym)
+        assert np.allclose(lam, Ap.omega / lmin, rtol=1e-15)
+        for j in range(t):
+            g = -Ap.alpha[j] / lmin
+            if sym:
+                w, Q = np.linalg.eigh(np.tril(H) + np.tril(H, -1).T)
+                E = (Q * np.exp(g * w)) @ Q.T
+            else:
+                E = scipy.linalg.expm(g * H)
+            for s in range(d):
+                ref = E @ bt[s]
+                assert np.abs(Ys[s][:, j] - ref).max() <= 1e-11 * max(1.0, np.abs(ref).max())
+
+
+def test_native_eigensolver_degenerate_spectrum():
+    """Repeated eigenvalues (identity blocks, the Laplace minors' symmetry) and a diagonal
+    matrix: exp(gS) b is still exact to rounding."""
+    k = 40
+    S = np.kron(np.eye(4), O.laplace_dense(10)[:10, :10] / 1e4)     # 4 repeated copies
+    bt = [np.random.default_rng(3).standard_normal(k)]
+
+    class Ap:
+        alpha = np.array([0.5])
+        omega = np.array([1.0])
+    lam, Ys = tkamd.solve_compressed_system(S, bt, Ap, 1.0, True)
+    w, Q = np.linalg.eigh(S)
+    ref = (Q * np.exp(-0.5 * w)) @ Q.T @ bt[0]
+    assert np.abs(Ys[0][:, 0] - ref).max() <= 1e-13
+    D = np.diag(np.arange(1.0, k + 1))
+    lam, Ys = tkamd.solve_compressed_system(D, bt, Ap, 1.0, True)
+    assert np.abs(Ys[0][:, 0] - np.exp(-0.5 * np.arange(1.0, k + 1)) * bt[0]).max() <= 1e-15
+
+
+def test_native_residual_breakdown_status():
+    """tk_residualnorm returns TK_BREAKDOWN with r_comp set (the reference throws
+    CompressedNormBreakdown, src/utils.jl:395)."""
+    import ctypes
+    lib = L.lib()
+    d, k, t = 1, 3, 2
+    H = np.eye(k).T.copy()
+    Y = np.zeros((d, t, k))
+    Y[0, :, 0] = 1.0
+    lam = np.ones(t)
+    B = np.zeros((d, k))
+    rc, rn = ctypes.c_double(), ctypes.c_double()
+    st = lib.tk_residualnorm(d, k, t, L.dptr(H), L.dptr(lam), L.dptr(Y), L.dptr(np.zeros(d)), L.dptr(B),
+                             ctypes.c_double(10.0), ctypes.byref(rc), ctypes.byref(rn))
+    assert st == L.TK_BREAKDOWN and rc.value < 0
+    assert lib.tk_residualnorm(0, k, t, None, None, None, None, None, 1.0, None, None) == 1   # TK_ERR_ARG
