@@ -310,9 +310,8 @@ def exchange_uid(tkamd, rank, timeout=120.0):
 
 
 def cpu_baseline(csc, n, d, K, seconds):
-    """The oracle's per-factor Arnoldi step timed on the host, on a bounded sample:
-    one factor of the same workload, steps k = 1, 2, ... until `seconds` elapse; the
-    per-k times are extrapolated (linear in k) to the K-step sweep of all d factors."""
+    """The C restatement's K-step Arnoldi sweeps timed on one host core, on a bounded
+    sample of the workload's factors (oracle/tk_ref.py baseline())."""
     try:
         sys.path.insert(0, ROOT)
         from oracle import tk_ref
