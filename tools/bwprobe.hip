@@ -139,6 +139,69 @@ __global__ __launch_bounds__(TPB) void k_pass2(Args a) {
     }
 }
 
+
+// double-buffered: the next tile's row is loaded before this tile's compute + reduction
+template <int MAXC>
+__device__ __forceinline__ void ld_row(double (&v)[MAXC], const Args& a, int f, int tile, int64_t TS) {
+    const double* Vt = a.V + ((int64_t)f * a.ntiles + tile) * TS;
+    const rsrc_t tv = mkrsrc(Vt, (uint32_t)((a.nc + 1) / 2) * TPB * 16);
+    const uint32_t toff = threadIdx.x * 16u;
+#pragma unroll
+    for (int c = 0; c < MAXC; c += 2) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 x = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(tv, toff + (uint32_t)(c / 2) * (TPB * 16), 0, 2));
+        v[c] = x.x;
+        v[c + 1] = x.y;
+    }
+}
+template <int MAXC>
+__device__ __forceinline__ void do_tile(const double (&v)[MAXC], const Args& a, int f, int tile, const double* hs,
+                                        double* tr, double* acc, bool first) {
+    const int64_t r = (int64_t)tile * TPB + threadIdx.x;
+    const double w = GP(const double, a.W)[f * a.ld + r];
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) s += v[c] * hs[c];
+    const double u = w - s;
+    GP(double, a.U)[f * a.ld + r] = u;
+#pragma unroll
+    for (int c0 = 0; c0 < MAXC; c0 += CH) {
+        if (c0 < a.nc) {
+            double x[CH];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) x[q] = c0 + q < MAXC ? v[c0 + q < MAXC ? c0 + q : 0] * u : 0.0;
+            chunk_reduce(x, tr, acc, c0, first);
+        }
+    }
+}
+template <int MAXC>
+__global__ __launch_bounds__(TPB) void k_pass2_db(Args a) {
+    __shared__ double tr[CH * TSTR];
+    __shared__ double hs[64];
+    __shared__ double acc[80];
+    const int f = blockIdx.y;
+    const int64_t TS = (int64_t)TPB * a.KC;
+    for (int c = threadIdx.x; c < 64; c += TPB) hs[c] = c < a.nc ? a.h[c] : 0.0;
+    __syncthreads();
+    double A[MAXC], B[MAXC];
+    int tile = blockIdx.x;
+    bool first = true;
+    if (tile < a.ntiles) ld_row<MAXC>(A, a, f, tile, TS);
+    for (; tile < a.ntiles; tile += 2 * a.npart) {
+        const int t2 = tile + a.npart, t3 = t2 + a.npart;
+        if (t2 < a.ntiles) ld_row<MAXC>(B, a, f, t2, TS);
+        do_tile<MAXC>(A, a, f, tile, hs, tr, acc, first);
+        first = false;
+        if (t2 < a.ntiles) {
+            if (t3 < a.ntiles) ld_row<MAXC>(A, a, f, t3, TS);
+            do_tile<MAXC>(B, a, f, t2, hs, tr, acc, false);
+        }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.nc; c += TPB)
+        GP(double, a.P)[((int64_t)f * 64 + c) * a.npart + blockIdx.x] = acc[c];
+}
+
 // pure read of the same bytes with 16 B/lane loads (flat column-contiguous sweep)
 __global__ __launch_bounds__(TPB) void k_read(const double2* __restrict__ p, int64_t n2, double* out) {
     double s = 0.0;
@@ -170,7 +233,7 @@ static float timeit(F f, int reps) {
 
 int main(int argc, char** argv) {
     const int nc = argc > 1 ? atoi(argv[1]) : 40;
-    const int nf = 8, KC = 51, ntiles = 4096;
+    const int nf = 8, KC = 52, ntiles = 4096;
     const int64_t ld = (int64_t)ntiles * TPB;
     Args a;
     const size_t vbytes = (size_t)nf * ntiles * KC * TPB * 8;
@@ -193,33 +256,23 @@ int main(int argc, char** argv) {
     auto rep = [&](const char* name, float ms) {
         printf("%-44s nc=%2d  %8.1f us  %6.2f TB/s\n", name, nc, ms * 1e3, bytes / (ms * 1e-3) / 1e12);
     };
-    for (int npart : {1024, 4096}) {
+    a.KC = 52;   // paired layout needs an even column count
+    for (int npart : {1024, 512}) {
         a.npart = npart;
         dim3 g(npart, nf);
         char nm[128];
-        const int KC0 = a.KC;
-        snprintf(nm, sizeof nm, "tile KC=51 MAXC48 nt        npart=%d", npart);
-        rep(nm, timeit([&] { k_pass2<48, 1, 2><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "tile KC=51 MAXC16 nt        npart=%d", npart);
-        if (nc <= 16) rep(nm, timeit([&] { k_pass2<16, 1, 2><<<g, TPB>>>(a); }, 20));
-        a.KC = nc;
-        snprintf(nm, sizeof nm, "tile KC=nc MAXC48 nt        npart=%d", npart);
-        rep(nm, timeit([&] { k_pass2<48, 1, 2><<<g, TPB>>>(a); }, 20));
-        a.KC = KC0;
-        snprintf(nm, sizeof nm, "paired16B MAXC48 nt         npart=%d", npart);
-        rep(nm, timeit([&] { k_pass2<48, 1, 2, 2><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "paired16B MAXC16 nt         npart=%d", npart);
+        snprintf(nm, sizeof nm, "paired MAXC48 single  npart=%d", npart);
+        if (nc > 16) rep(nm, timeit([&] { k_pass2<48, 1, 2, 2><<<g, TPB>>>(a); }, 20));
+        snprintf(nm, sizeof nm, "paired MAXC48 dbuf    npart=%d", npart);
+        if (nc > 16) rep(nm, timeit([&] { k_pass2_db<48><<<g, TPB>>>(a); }, 20));
+        snprintf(nm, sizeof nm, "paired MAXC16 single  npart=%d", npart);
         if (nc <= 16) rep(nm, timeit([&] { k_pass2<16, 1, 2, 2><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "paired16B MAXC40 nt         npart=%d", npart);
-        if (nc <= 40) rep(nm, timeit([&] { k_pass2<40, 1, 2, 2><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "tile MAXC40 nt              npart=%d", npart);
-        if (nc <= 40) rep(nm, timeit([&] { k_pass2<40, 1, 2, 0><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "colmajor MAXC48 nt          npart=%d", npart);
-        rep(nm, timeit([&] { k_pass2<48, 1, 2, 1><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "colmajor MAXC48 default     npart=%d", npart);
-        rep(nm, timeit([&] { k_pass2<48, 1, 0, 1><<<g, TPB>>>(a); }, 20));
-        snprintf(nm, sizeof nm, "colmajor MAXC16 nt          npart=%d", npart);
-        if (nc <= 16) rep(nm, timeit([&] { k_pass2<16, 1, 2, 1><<<g, TPB>>>(a); }, 20));
+        snprintf(nm, sizeof nm, "paired MAXC16 dbuf    npart=%d", npart);
+        if (nc <= 16) rep(nm, timeit([&] { k_pass2_db<16><<<g, TPB>>>(a); }, 20));
+        snprintf(nm, sizeof nm, "paired MAXC8 single   npart=%d", npart);
+        if (nc <= 8) rep(nm, timeit([&] { k_pass2<8, 1, 2, 2><<<g, TPB>>>(a); }, 20));
+        snprintf(nm, sizeof nm, "paired MAXC8 dbuf     npart=%d", npart);
+        if (nc <= 8) rep(nm, timeit([&] { k_pass2_db<8><<<g, TPB>>>(a); }, 20));
     }
     {
         // whole-V read with nontemporal 16 B loads: same byte count as nc columns over all tiles
