@@ -48,11 +48,18 @@ CONFIGS = {
 }
 
 
-def alg_bytes_step(n, nnz, k):
-    """algorithmic bytes of one Arnoldi factor-step with k basis columns
-    (int32 CSR): B_spmv + 2 MGS passes + write V_{k+1} + the RHS dot."""
+def alg_bytes_step(n, nnz, k, method="TensorArnoldi"):
+    """algorithmic bytes of one factor-step with k basis columns (int32 CSR).
+    Arnoldi: B_spmv + 2 MGS passes + write V_{k+1} + the RHS dot.  Lanczos: B_spmv + read
+    V_{k-1} + write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new
+    column, 8n(k+1) (its redo steps are extra work, not counted)."""
     b_spmv = 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n
-    return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
+    if method == "TensorArnoldi":
+        return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
+    b = b_spmv + 8 * n + 8 * n + 8 * n
+    if method == "TensorLanczosReorth":
+        b += 8 * n * (k + 1)
+    return b
 
 
 def main():
@@ -61,6 +68,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--method", default=None, choices=["TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"],
+                    help="orthonormalization type (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--force-comm", action="store_true",
@@ -87,6 +96,8 @@ def main():
             sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
 
     d, n, cls, method, K, inst = CONFIGS[args.config]
+    if args.method:
+        method = args.method
     ctx = tkamd.Context(local_rank)
     part = tkamd.Partition(d, world, rank)
     if args.emulate_ranks > 1 and world == 1:
@@ -107,7 +118,9 @@ def main():
     for s in part.local():
         b = np.random.default_rng(1000 + s).random(n)
         bs.append(b / np.linalg.norm(b))
-    dev = tkamd.DeviceDecomposition(ctx, L.TK_ARNOLDI if method == "TensorArnoldi" else L.TK_LANCZOS,
+    mcode = {"TensorArnoldi": L.TK_ARNOLDI, "TensorLanczos": L.TK_LANCZOS,
+             "TensorLanczosReorth": L.TK_LANCZOS_REORTH}[method]
+    dev = tkamd.DeviceDecomposition(ctx, mcode,
                                     d, part.first, [A] * part.nf, bs, K)
     # exp-sum rank at k = K (Laplace: kappa independent of n and d)
     sym = inst == "SymInstance"
@@ -212,7 +225,7 @@ def main():
     iters = K * args.steps
     value = iters / elapsed
     # roofline of the Arnoldi step (SpMV + MGS2 + reductions), device time from events
-    alg_step = sum(alg_bytes_step(n, nnz, k) for k in range(1, K + 1)) * part.nf
+    alg_step = sum(alg_bytes_step(n, nnz, k, method) for k in range(1, K + 1)) * part.nf
     step_avg_s = (step_ms / 1e3) / max(step_cnt, 1)
     achieved = (alg_step / K) / step_avg_s / 1e9 if step_cnt else None
     vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
@@ -223,7 +236,7 @@ def main():
     if rank == 0:
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
-        if os.path.exists(pmc_path) and not args.emulate_ranks:
+        if os.path.exists(pmc_path) and not args.emulate_ranks and method == CONFIGS[args.config][3]:
             try:
                 traffic = json.load(open(pmc_path)).get("hbm_bytes_per_step")
             except Exception:
@@ -254,7 +267,10 @@ def main():
                                       % (world, ", forced on 1 rank" if args.force_comm else "")},
             "roofline": {
                 "bound": "hbm",
-                "kernel": "Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors",
+                "kernel": ("Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors"
+                           if method == "TensorArnoldi" else
+                           "%s factor-step (TTR SpMV pass, update pass, reduces, post%s), all local factors"
+                           % (method, ", Gram row + host loss check" if method == "TensorLanczosReorth" else "")),
                 "achieved": round(achieved, 1) if achieved else None,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

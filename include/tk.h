@@ -143,8 +143,9 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out);
 tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out);
 
 /* Enqueue steps j0 .. j1-1 back to back with no host synchronisation (the device
- * iteration of the driver loop, src/tensor_krylov_method.jl:63-66).  TK_LANCZOS_REORTH
- * takes its loss check as a host decision per step, so its sweep waits once per step. */
+ * iteration of the driver loop, src/tensor_krylov_method.jl:63-66).  All three methods
+ * run asynchronously: TK_LANCZOS_REORTH takes its loss check and MGS-redo decision on the
+ * device (src/orthogonal_bases.jl:119-131). */
 tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1);
 
 /* Write the last pending basis column V[:, j+1] (the fused pipeline defers it into

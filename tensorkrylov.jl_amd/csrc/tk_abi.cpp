@@ -526,15 +526,12 @@ struct tk_decomp {
     std::vector<tk_mat*> mats;
     std::vector<DFac> hf;   // host copy of descriptors
     DFac* df = nullptr;     // device descriptors
-    DFac* dsub = nullptr;   // scratch descriptor array (LanczosReorth redo subset)
     std::vector<void*> allocs;
     double* rec = nullptr;   // send records [(kmax+2) slots][d_total][m] (local rows only)
     double* recv = nullptr;  // all-reduced records (== rec on a single rank)
     double* Ydev = nullptr; size_t ycap = 0;
     double* Xdev = nullptr; size_t xcap = 0;
     double* scratch = nullptr;   // column gather buffer (n x 8)
-    // host Gram mirror (LanczosReorth decisions): [nf][(kmax+1)^2]
-    std::vector<std::vector<double>> gram;
     // per-slot events: compute -> exchange (slot written) and exchange -> compute
     // (the all-reduce has finished reading the slot's send rows)
     std::vector<hipEvent_t> ev_c, ev_x;
@@ -624,6 +621,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.h2, (KP + 16) * sizeof(double));   // + COEF_TAIL (tk_kernels.hip)
         DA(d.g, (KP + 16) * sizeof(double));
         DA(d.H, (size_t)KP * KC * sizeof(double));
+        DA(d.lossrow, (size_t)KP * sizeof(double));
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
@@ -635,7 +633,6 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;
     }
     DA(dc->df, nf * sizeof(DFac));
-    DA(dc->dsub, nf * sizeof(DFac));
     {
         hipError_t e = hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice);
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
@@ -649,7 +646,6 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     else
         dc->recv = dc->rec;
 #undef DA
-    if (method == TK_LANCZOS_REORTH) dc->gram.assign(nf, std::vector<double>((size_t)KC * KC, 0.0));
     if (dc->recv != dc->rec) {
         dc->ev_c.assign(kmax + 2, nullptr);
         dc->ev_x.assign(kmax + 2, nullptr);
@@ -699,6 +695,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.m = dc->m;
     a.rec = dc->rec + (size_t)slot * dc->d_total * dc->m;
     a.fmt = dc->fmt;
+    a.gate = 0;
     return a;
 }
 
@@ -764,16 +761,6 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
     dc->jnext = 0;
     dc->pending = false;
     dc->last_j = -1;
-    if (dc->method == TK_LANCZOS_REORTH) {
-        // G[0,0] for the host loss mirror
-        std::vector<double> r((size_t)dc->d_total * dc->m);
-        st = exchange_and_copy(dc, 0, r.data());
-        if (st) return st;
-        for (int f = 0; f < nf; ++f)
-            dc->gram[f][0] = r[(size_t)(dc->foff + f) * dc->m + rec_gram(dc->kmax)];
-        if (rec_out) memcpy(rec_out, r.data(), r.size() * sizeof(double));
-        return TK_OK;
-    }
     return exchange_and_copy(dc, 0, rec_out);
 }
 
@@ -794,16 +781,6 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
     return TK_OK;
 }
 
-static double gram_loss(const std::vector<double>& G, int KC, int ncols) {
-    // ||G[0..ncols) - I||_F with G symmetric, rows stored as G[c*KC + i], i <= c
-    double s = 0.0;
-    for (int cidx = 0; cidx < ncols; ++cidx)
-        for (int i = 0; i <= cidx; ++i) {
-            const double v = G[(size_t)cidx * KC + i] - (i == cidx ? 1.0 : 0.0);
-            s += (i == cidx ? 1.0 : 2.0) * v * v;
-        }
-    return sqrt(s);
-}
 
 static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_ctx* c = dc->ctx;
@@ -839,8 +816,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else {
-        // TensorLanczosReorth (src/orthogonal_bases.jl:98-139): TTR, write v_{j+1},
-        // host loss check, MGS redo of step j for the factors that need it.
+        // TensorLanczosReorth (src/orthogonal_bases.jl:98-139): TTR, write v_{j+1} with its
+        // Gram row, the loss check on the device (post LAN_FIN sets SC_REDO per factor),
+        // then the MGS redo of step j as gated launches: blocks of factors whose flag is
+        // clear return at once.  No host round trip, so the step can be swept.
         RUN(TCLS_PASS1, 2, launch_lan_l1_plain(dc->df, nf, a, s), "lan_l1_plain");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
         RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
@@ -848,58 +827,17 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, 0, 1, s), "post");
         RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, 0, s), "post");
-        const size_t cnt = (size_t)dc->d_total * dc->m;
-        std::vector<double> r(cnt);
-        double* slotp = a.rec;
-        HIPCHK(hipMemcpyAsync(r.data(), slotp, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const int KC = dc->kmax + 1, kmax = dc->kmax, m = dc->m;
-        const double thr = sqrt(2.220446049250313e-16);
-        std::vector<int> redo(nf, 0);
-        std::vector<double> loss(nf, 0.0);
-        bool any = false;
-        for (int f = 0; f < nf; ++f) {
-            const double* rf = r.data() + (size_t)(dc->foff + f) * m;
-            for (int i = 0; i <= j + 1; ++i) dc->gram[f][(size_t)(j + 1) * KC + i] = rf[rec_gram(kmax) + i];
-            loss[f] = gram_loss(dc->gram[f], KC, j + 2);
-            redo[f] = loss[f] > thr;
-            any = any || redo[f];
-        }
-        if (any) {
-            // Redo step j with MGS for the selected factors: run the Arnoldi kernels on a
-            // descriptor array that contains only those factors.
-            std::vector<DFac> sub;
-            for (int f = 0; f < nf; ++f)
-                if (redo[f]) sub.push_back(dc->hf[f]);
-            DFac* dsub = dc->dsub;
-            HIPCHK(hipMemcpy(dsub, sub.data(), sub.size() * sizeof(DFac), hipMemcpyHostToDevice));
-            const int ns = (int)sub.size();
-            RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dsub, ns, a, s), "arn_a1_plain");
-            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 1, dc->npart, s), "reduce");
-            RUN(TCLS_PASS2, 2, launch_arn_a2(dsub, ns, a, s), "arn_a2");
-            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 2, 2 * j + 4, dc->npart, s), "reduce");
-            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN, 0, 1, s), "post");
-            RUN(TCLS_FIN, 2, launch_arn_finalize(dsub, ns, a, s), "arn_finalize");
-            RUN(TCLS_RED, 2, launch_reduce(dsub, ns, 1, j + 3, dc->npart, s), "reduce");
-            RUN(TCLS_RED, 2, launch_post(dsub, ns, a, POST_ARN_FIN, 0, 0, s), "post");
-            HIPCHK(hipMemcpyAsync(r.data(), slotp, cnt * sizeof(double), hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            for (int f = 0; f < nf; ++f) {
-                if (!redo[f]) continue;
-                const double* rf = r.data() + (size_t)(dc->foff + f) * m;
-                for (int i = 0; i <= j + 1; ++i) dc->gram[f][(size_t)(j + 1) * KC + i] = rf[rec_gram(kmax) + i];
-            }
-        }
-        // loss / flag fields for the local factors
-        for (int f = 0; f < nf; ++f) {
-            double* rf = r.data() + (size_t)(dc->foff + f) * m;
-            rf[rec_loss(kmax)] = loss[f];
-            rf[rec_flag(kmax)] = redo[f] ? 1.0 : 0.0;
-            HIPCHK(hipMemcpyAsync(slotp + (size_t)(dc->foff + f) * m + rec_loss(kmax), rf + rec_loss(kmax),
-                                  2 * sizeof(double), hipMemcpyHostToDevice, s));
-        }
-        HIPCHK(hipStreamSynchronize(s));
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 1, 0, s), "post");
+        KArgs g = a;
+        g.gate = 1;
+        RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, g, s), "arn_a1_plain");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s, 1), "reduce");
+        RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, g, s), "arn_a2");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s, 1), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, g, POST_ARN, 0, 0, s), "post");
+        RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, g, s), "arn_finalize");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s, 1), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, g, POST_ARN_FIN, 0, 0, s), "post");
         dc->pending = false;
     }
     dc->last_j = j;
@@ -920,8 +858,6 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
 
 tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
     CHECKARG(dc, "NULL decomp");
-    // (LanczosReorth steps take their redo decision on the host inside tk_decomp_step,
-    // so its sweep synchronizes once per step; Arnoldi / Lanczos sweeps never wait)
     for (int j = j0; j < j1; ++j) {
         tk_status st = tk_decomp_step(dc, j, nullptr);
         if (st) return st;

@@ -14,6 +14,7 @@ enum {
     SC_BETAPREV = 2,  // Lanczos beta_{j-1} for a plain (non-fused) TTR step
     SC_INVB = 3,      // inv(norm(b))
     SC_BNORM = 4,     // norm(b)
+    SC_REDO = 5,      // LanczosReorth: 1 when this step's loss check asks for the MGS redo
     SC_COUNT = 8
 };
 
@@ -56,6 +57,7 @@ struct DFac {
     double* h2;           // second-pass coefficients of the last Arnoldi step (kmax+2)
     double* g;            // Hbar * h2 (kmax+2)
     double* H;            // Hessenberg, column-major (kmax+2) x (kmax+1)
+    double* lossrow;      // per column c: its share of ||V'V - I||_F^2 (LanczosReorth loss check)
     int track_gram;       // keep Gram rows for this factor
     int gidx;             // global factor index (record slot)
 };
@@ -70,6 +72,7 @@ struct KArgs {
     int m;            // record length per factor
     double* rec;      // record slot base ([d_total][m])
     int fmt;          // storage common to all factors of the launch: 1 DIA, 2 SELL, 3 CSR, 0 mixed
+    int gate;         // 1: a block does nothing unless its factor's SC_REDO flag is set
 };
 
 // launchers (tk_kernels.hip)
@@ -83,7 +86,7 @@ void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
-void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s);
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0);
 // post-processing (one 64-thread block per factor)
 enum PostKind {
     POST_INIT_A = 0,

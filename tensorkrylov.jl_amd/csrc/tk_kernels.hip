@@ -319,6 +319,7 @@ __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
     __shared__ double tr[CH * TSTR];                                   \
     extern __shared__ __attribute__((aligned(16))) double lds[];       \
     const DFac& d = F[blockIdx.y];                                     \
+    if (a.gate && ld(d.sc, SC_REDO) == 0.0) return;                    \
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);                     \
     (void)TS;
 
@@ -587,10 +588,11 @@ __global__ __launch_bounds__(TPB) void k_lan_finalize(const DFac* __restrict__ F
 
 // RED[c] = sum_b P[c*npart + b]: one wave per value, fixed order (16 independent
 // strided loads per lane, then a fixed-order combine).
-__global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int which, int nv, int npart) {
+__global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int which, int nv, int npart, int gate) {
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
     if (c >= nv) return;
+    if (gate && ld(d.sc, SC_REDO) == 0.0) return;
     const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
     const int l = threadIdx.x;
     double part[16];
@@ -622,6 +624,18 @@ __device__ __forceinline__ void put_gram(double* rec, int kmax, int c, const dou
         st(rec, rec_col(kmax), (double)c);
         st(rec, rec_tracked(kmax), tracked ? 1.0 : 0.0);
     }
+}
+
+// Column c's share of ||V'V - I||_F^2 from its Gram row g[0..c] (g[i] = <V[:,i], V[:,c]>):
+// off-diagonal entries count twice (the Gram matrix is symmetric).
+__device__ __forceinline__ double loss_row(const double* g, int c) {
+    double s = 0.0;
+    for (int i = 0; i < c; ++i) {
+        const double v = ld(g, i);
+        s += 2.0 * v * v;
+    }
+    const double dv = ld(g, c) - 1.0;
+    return s + dv * dv;
 }
 
 #define POST_LDS_MAX 8192   // doubles of dynamic LDS for Hbar in k_post (kmax <= 88)
@@ -690,6 +704,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     __shared__ double h2s[1024 + 8];
     extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
+    if (a.gate && ld(d.sc, SC_REDO) == 0.0) return;
     const int j = a.j, kmax = a.kmax;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
     const int t = threadIdx.x;
@@ -714,6 +729,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     }
     if (kind == POST_INIT_B) {
         put_gram(rec, kmax, 0, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
+        if (t == 0 && d.track_gram) st(d.lossrow, 0, loss_row(d.RED1 + 1, 0));
         return;
     }
     if (kind == POST_ARN) {
@@ -724,6 +740,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_ARN_FIN) {
         // RED1 = [gram_{j+1} (j+2) | bt]
         put_gram(rec, kmax, j + 1, d.RED1, ld(d.RED1, j + 2), d.track_gram);
+        if (t == 0 && d.track_gram) st(d.lossrow, j + 1, loss_row(d.RED1, j + 1));   // (redone column)
         return;
     }
     if (kind == POST_LAN) {
@@ -745,6 +762,20 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_LAN_FIN) {
         // RED1 = [bt | gram_{j+1} (j+2)]
         put_gram(rec, kmax, j + 1, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
+        if (t == 0 && d.track_gram) {
+            st(d.lossrow, j + 1, loss_row(d.RED1 + 1, j + 1));
+            if (flag) {
+                // LanczosReorth loss check (src/orthogonal_bases.jl:119-123):
+                // loss = ||V[:,1:k+1]'V[:,1:k+1] - I||_F, MGS redo when loss > sqrt(eps)
+                double s2 = 0.0;
+                for (int c = 0; c <= j + 1; ++c) s2 += ld(d.lossrow, c);
+                const double loss = sqrt(s2);
+                const bool redo = loss > 1.4901161193847656e-8;   // sqrt(eps(Float64))
+                st(rec, rec_loss(kmax), loss);
+                st(rec, rec_flag(kmax), redo ? 1.0 : 0.0);
+                st(d.sc, SC_REDO, redo ? 1.0 : 0.0);
+            }
+        }
         return;
     }
 }
@@ -941,8 +972,8 @@ void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
-void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s) {
-    hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart);
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate) {
+    hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
