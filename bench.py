@@ -48,12 +48,18 @@ CONFIGS = {
 }
 
 
-def alg_bytes_step(n, nnz, k, method="TensorArnoldi"):
+def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None):
     """algorithmic bytes of one factor-step with k basis columns (int32 CSR).
-    Arnoldi: B_spmv + 2 MGS passes + write V_{k+1} + the RHS dot.  Lanczos: B_spmv + read
-    V_{k-1} + write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new
+    Arnoldi as two-sweep CGS2 (sweeps=2): B_spmv + 2 MGS passes + write V_{k+1} + the RHS
+    dot.  One-sweep Arnoldi (sweeps=1, delayed reorthogonalization):
+    V_1..V_{k-1} read once + the raw vector u read and written + V_k written + b read
+    (both SpMVs take their vector from LDS) + the matrix bytes its storage must read
+    (`mat_bytes`: 0 for a Toeplitz band, whose diagonals are 4 scalars).  Lanczos: B_spmv +
+    read V_{k-1} + write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new
     column, 8n(k+1) (its redo steps are extra work, not counted)."""
     b_spmv = 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n
+    if method == "TensorArnoldi" and sweeps == 1:
+        return 8 * n * (k - 1) + 4 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
     if method == "TensorArnoldi":
         return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
     b = b_spmv + 8 * n + 8 * n + 8 * n
@@ -135,6 +141,7 @@ def main():
         t_rank = 17 if sym else 3
     rng = np.random.default_rng(7)
     Ys = [rng.standard_normal((K, t_rank)) for _ in range(part.nf)]
+    sweeps = dev.arnoldi_sweeps if method == "TensorArnoldi" else 0
 
     host_issue = [0.0, 0]
 
@@ -183,7 +190,8 @@ def main():
     sweep()
     ctx.sync()
     kern = {}
-    for name, cls_id in (("pass1_spmv_cgs", L.T_PASS1), ("pass2_cgs", L.T_PASS2), ("finalize", L.T_FIN),
+    p1name = "sweep_spmv2_dcgs2" if sweeps == 1 else "pass1_spmv_cgs"
+    for name, cls_id in ((p1name, L.T_PASS1), ("pass2_cgs", L.T_PASS2), ("finalize", L.T_FIN),
                          ("reduce_post", L.T_RED), ("basis_mul", L.T_VY), ("exchange", L.T_XCH)):
         ms, cnt = ctx.timing_read(cls_id)
         kern[name] = {"avg_us": round(1e3 * ms / cnt, 3) if cnt else None, "launches": cnt}
@@ -225,7 +233,8 @@ def main():
     iters = K * args.steps
     value = iters / elapsed
     # roofline of the Arnoldi step (SpMV + MGS2 + reductions), device time from events
-    alg_step = sum(alg_bytes_step(n, nnz, k, method) for k in range(1, K + 1)) * part.nf
+    alg_step = sum(alg_bytes_step(n, nnz, k, method, sweeps, toeplitz_bytes(csc))
+                   for k in range(1, K + 1)) * part.nf
     step_avg_s = (step_ms / 1e3) / max(step_cnt, 1)
     achieved = (alg_step / K) / step_avg_s / 1e9 if step_cnt else None
     vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
@@ -267,7 +276,10 @@ def main():
                                       % (world, ", forced on 1 rank" if args.force_comm else "")},
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors"
+                "kernel": ("one-sweep Arnoldi factor-step (k_arn_d1: v_j, two SpMVs from LDS, CGS projections "
+                           "with the reorthogonalization delayed one step; 1 reduce, post), all local factors"
+                           if method == "TensorArnoldi" and sweeps == 1 else
+                           "Arnoldi factor-step (pass1 SpMV+CGS fused, pass2 CGS, 2 reduce, post), all local factors"
                            if method == "TensorArnoldi" else
                            "%s factor-step (TTR SpMV pass, update pass, reduces, post%s), all local factors"
                            % (method, ", Gram row + host loss check" if method == "TensorLanczosReorth" else "")),
@@ -277,6 +289,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg_step / K,
+                "arnoldi_sweeps_over_V": sweeps if method == "TensorArnoldi" else None,
                 "avg_launch_us": round(step_avg_s * 1e6, 2),
             },
             "host_issue_us_per_iteration": round(host_us_per_step, 2),
@@ -300,6 +313,21 @@ def main():
     dev.close()
     A.close()
     ctx.close()
+
+
+def toeplitz_bytes(csc):
+    """Matrix bytes a one-sweep factor-step must read: 0 when every diagonal of the band is
+    constant (the device keeps them as scalars), else the DIA values (8 B per stored
+    entry, the band's nonzeros)."""
+    colptr, rowval, nzval = csc
+    n = len(colptr) - 1
+    cols = np.repeat(np.arange(n), np.diff(colptr))
+    off = cols - rowval
+    for o in np.unique(off):
+        v = nzval[off == o]
+        if len(v) != n - abs(int(o)) or not np.all(v == v[0]):
+            return 8 * len(nzval)
+    return 0
 
 
 def exchange_uid(tkamd, rank, timeout=120.0):

@@ -117,6 +117,12 @@ tk_status tk_decomp_create(tk_ctx* ctx, int method, int d_total, int first_facto
                            int track_all_gram, tk_decomp** out);
 tk_status tk_decomp_destroy(tk_decomp* dc);
 
+/* Sweeps over V per TK_ARNOLDI step: 1 = CGS2 with the reorthogonalization delayed by one
+ * step (every local A_s banded, DIA with bandwidths <= 4), 2 = CGS2
+ * (other storage, or TKHIP_ARNOLDI=cgs2 in the environment at create); 0 for the
+ * Lanczos methods. */
+int tk_decomp_arnoldi_sweeps(tk_decomp* dc);
+
 /* Per-factor record layout (doubles; m = tk_record_len(kmax)), written by every step:
  *   [0 .. kmax+1]        H[0..j+1, j] as computed by this step (rest 0)
  *   [kmax+2 .. 2kmax+3]  Gram row G[c, 0..c] = V[:,c]' V[:,0..c] of column c below

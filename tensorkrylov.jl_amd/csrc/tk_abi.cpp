@@ -229,6 +229,7 @@ struct tk_mat {
     int64_t dld = 0;
     double* dconst = nullptr;
     int toep = 0;
+    int hl = 0, hu = 0;   // lower / upper bandwidth of the DIA storage
     long long* sptr = nullptr;
     int* swidth = nullptr;
     int* rowlen = nullptr;
@@ -386,6 +387,8 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
     if (e == hipSuccess && A->nnz) e = hipMemcpy(A->val, v.data(), A->nnz * sizeof(double), hipMemcpyHostToDevice);
     if (e == hipSuccess && !offs.empty()) {
         A->ndiag = (int)offs.size();
+        A->hl = std::max(0, -offs.front());
+        A->hu = std::max(0, offs.back());
         offs.resize(dia_rows(A->ndiag), 0);
         e = hipMalloc(&A->doff, offs.size() * sizeof(int));
         if (e == hipSuccess) e = hipMalloc(&A->dval, dv.size() * sizeof(double));
@@ -520,6 +523,8 @@ struct tk_decomp {
     int ntiles, npart;
     int jnext = 0;          // next step index
     int fmt = 0;            // SpMV storage shared by all local factors (KArgs::fmt)
+    bool onesweep = false;  // Arnoldi as one sweep per step (k_arn_d1): banded A_s only
+    int npd = 0;            // max DFac::npd over the local factors (grid width of k_arn_d1)
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
     int last_j = -1;
@@ -585,12 +590,30 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     dc->ntiles = (int)((n + 255) / 256);
     // partial count: a function of n only (bitwise results independent of the factor
     // partition); TKHIP_NPART overrides it for tuning experiments
+    int npcap = 1024;
     {
         const char* e = getenv("TKHIP_NPART");
-        const int cap = e ? std::max(32, atoi(e)) : 1024;
-        dc->npart = std::min(dc->ntiles, cap);
+        npcap = e ? std::max(32, atoi(e)) : 1024;
+        dc->npart = std::min(dc->ntiles, npcap);
     }
-    dc->nvmax = 2 * kmax + 8;
+    {
+        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? (A->toep ? 5 : 1) : 4) : (A->sell ? 2 : 3); };
+        dc->fmt = fmt_of(mats[0]);
+        for (int f = 1; f < nf; ++f)
+            if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;
+    }
+    // Arnoldi runs as one sweep per step (k_arn_d1) when every local factor is banded
+    // (DIA, bandwidths <= 4: the SpMVs read their vector from the window in LDS) and its
+    // basis is addressable with 31-bit offsets; TKHIP_ARNOLDI=cgs2 keeps the two-sweep CGS2.
+    {
+        const char* e = getenv("TKHIP_ARNOLDI");
+        bool ok = method == TK_ARNOLDI && !(e && strcmp(e, "cgs2") == 0) && (dc->fmt == 1 || dc->fmt == 5);
+        const double vbytes = (double)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double);
+        ok = ok && vbytes < 2147483648.0 - 1048576.0;
+        for (int f = 0; ok && f < nf; ++f) ok = mats[f]->hl <= 4 && mats[f]->hu <= 4;
+        dc->onesweep = ok;
+    }
+    dc->nvmax = dc->onesweep ? 3 * kmax + 8 : 2 * kmax + 8;
     dc->mats.assign(mats, mats + nf);
     dc->hf.resize(nf);
     const int KP = kmax + 2, KC = kmax + 1;
@@ -605,6 +628,19 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     for (int f = 0; f < nf; ++f) {
         DFac& d = dc->hf[f];
         d.A = mats[f]->spm();
+        d.hl = mats[f]->hl;
+        d.hu = mats[f]->hu;
+        {
+            // overlapping windows of 256 rows owning 256 - 2(hl+hu); partial blocks a
+            // function of (n, hl, hu) only, each walking the same number of windows
+            const int ws = 256 - 2 * (d.hl + d.hu);
+            d.nwin = (int)((n + ws - 1) / ws);
+            const char* ew = getenv("TKHIP_D1_WPB");
+            const int wpb = TK_D1_ONEWIN ? 1 : (ew ? std::max(0, atoi(ew)) : 0);
+            d.npd = wpb >= 1 ? (d.nwin + wpb - 1) / wpb : (d.nwin + std::max(1, d.nwin / npcap) - 1) / std::max(1, d.nwin / npcap);
+        }
+        dc->npd = std::max(dc->npd, d.npd);
+        const int npp = std::max(dc->npart, dc->onesweep ? d.npd : 0);
         DA(d.V, (size_t)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double));   // tile-major, paired columns
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
@@ -613,8 +649,8 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.b = bb;
         DA(d.W, (size_t)dc->ld * sizeof(double));
         DA(d.U, (size_t)dc->ld * sizeof(double));
-        DA(d.P1, (size_t)dc->nvmax * dc->npart * sizeof(double));
-        DA(d.P2, (size_t)dc->nvmax * dc->npart * sizeof(double));
+        DA(d.P1, (size_t)dc->nvmax * npp * sizeof(double));
+        DA(d.P2, (size_t)dc->nvmax * npp * sizeof(double));
         DA(d.RED1, (size_t)dc->nvmax * sizeof(double));
         DA(d.RED2, (size_t)dc->nvmax * sizeof(double));
         DA(d.sc, SC_COUNT * sizeof(double));
@@ -625,12 +661,6 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
-    }
-    {
-        auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? (A->toep ? 5 : 1) : 4) : (A->sell ? 2 : 3); };
-        dc->fmt = fmt_of(mats[0]);
-        for (int f = 1; f < nf; ++f)
-            if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;
     }
     DA(dc->df, nf * sizeof(DFac));
     {
@@ -662,6 +692,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     for (tk_mat* A : dc->mats) A->refs++;
     *out = dc;
     return TK_OK;
+}
+
+int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
+    if (!dc || dc->method != TK_ARNOLDI) return 0;
+    return dc->onesweep ? 1 : 2;
 }
 
 tk_status tk_decomp_destroy(tk_decomp* dc) {
@@ -696,6 +731,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.rec = dc->rec + (size_t)slot * dc->d_total * dc->m;
     a.fmt = dc->fmt;
     a.gate = 0;
+    a.ubuf = 0;
     return a;
 }
 
@@ -754,9 +790,15 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
     RUN(TCLS_PASS1, 2, launch_init_a(dc->df, nf, a, s), "init_a");
     RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 1, dc->npart, s), "reduce");
     RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_A, 0, 0, s), "post");
-    RUN(TCLS_PASS1, 2, launch_init_b(dc->df, nf, a, s), "init_b");
-    RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2, dc->npart, s), "reduce");
-    RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, 1, s), "post");
+    if (dc->onesweep) {
+        RUN(TCLS_PASS1, 2, launch_init_bd(dc->df, nf, a, dc->npd, s), "init_bd");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3, 0, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 1, 1, s), "post");
+    } else {
+        RUN(TCLS_PASS1, 2, launch_init_b(dc->df, nf, a, s), "init_b");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 2, dc->npart, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, 1, s), "post");
+    }
     dc->inited = true;
     dc->jnext = 0;
     dc->pending = false;
@@ -770,7 +812,9 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
     hipStream_t s = c->stream;
     const int nf = dc->nf, j = a.j;
     if (dc->method == TK_ARNOLDI) {
-        RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, a, s), "arn_finalize");
+        KArgs f = a;
+        if (dc->onesweep && j <= D1_JMAX) f.ubuf = (j & 1) ? 0 : 1;   // one-sweep step j wrote u_{j+1} to U (j odd) or W
+        RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, f, s), "arn_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, 1, s), "post");
     } else {
@@ -790,7 +834,23 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     if (st) return st;
     KArgs a = base_args(dc, j, slot);
     Timer step_timer(c, TCLS_STEP, 1);
-    if (dc->method == TK_ARNOLDI) {
+    if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
+        // leaving the one-sweep range: write the pending column v_j (its record is
+        // overwritten by the CGS2 step below, which reports column j again)
+        tk_status st2 = finalize_pending(dc, base_args(dc, j - 1, slot));
+        if (st2) return st2;
+        dc->pending = false;
+    }
+    if (dc->method == TK_ARNOLDI && dc->onesweep && j <= D1_JMAX) {
+        // one sweep: writes v_j, u_{j+1}; reduce; post -> H column j and the next step's
+        // coefficients.  v_j is re-derived from (U or W, h2, inv_beta) whether or not a
+        // flush already wrote it (same operands, same order: the same value).
+        a.ubuf = j & 1;
+        RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, dc->npd, s), "arn_d1");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_D, 0, 1, s), "post");
+        dc->pending = true;
+    } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
         if (fused) {
             RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");

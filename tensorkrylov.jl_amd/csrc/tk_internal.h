@@ -60,6 +60,10 @@ struct DFac {
     double* lossrow;      // per column c: its share of ||V'V - I||_F^2 (LanczosReorth loss check)
     int track_gram;       // keep Gram rows for this factor
     int gidx;             // global factor index (record slot)
+    // one-sweep Arnoldi (k_arn_d1, banded A_s only): lower/upper bandwidth, overlapping
+    // row windows of stride 256 - 2(hl+hu), window count, partial blocks (a function of
+    // n, hl, hu only)
+    int hl, hu, nwin, npd;
 };
 
 struct KArgs {
@@ -73,7 +77,17 @@ struct KArgs {
     double* rec;      // record slot base ([d_total][m])
     int fmt;          // storage common to all factors of the launch: 1 DIA, 2 SELL, 3 CSR, 0 mixed
     int gate;         // 1: a block does nothing unless its factor's SC_REDO flag is set
+    int ubuf;         // one-sweep Arnoldi: 0 = the pending raw vector u is in U, 1 = in W
 };
+
+// One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
+// row); later steps of the same decomposition run as CGS2.
+constexpr int D1_JMAX = 64;
+// 1: each k_arn_d1 block takes one window (DFac::npd == nwin); 0: blocks walk windows
+// (TKHIP_D1_WPB per block; 0 = about 1024 blocks per factor)
+#ifndef TK_D1_ONEWIN
+#define TK_D1_ONEWIN 1
+#endif
 
 // launchers (tk_kernels.hip)
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);
@@ -82,10 +96,13 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+// npart <= 0: each factor's own DFac::npd partials (one-sweep Arnoldi)
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0);
 // post-processing (one 64-thread block per factor)
 enum PostKind {
@@ -94,7 +111,8 @@ enum PostKind {
     POST_ARN = 2,        // after a2; fused flag in `flag`
     POST_ARN_FIN = 3,    // after arn_finalize (column j+1)
     POST_LAN = 4,        // after l2; fused flag in `flag`
-    POST_LAN_FIN = 5     // after lan_finalize (column j+1)
+    POST_LAN_FIN = 5,    // after lan_finalize (column j+1)
+    POST_ARN_D = 6       // after k_arn_d1 (one-sweep Arnoldi): H column j, c, beta, next h1
 };
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s);
 void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s);

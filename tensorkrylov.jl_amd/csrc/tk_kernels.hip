@@ -112,6 +112,23 @@ __device__ __forceinline__ double row16_sum(double s) {
     return s;
 }
 
+// Reduce-scatter over each 16-lane row: lane l returns the sum over its row's 16 lanes of
+// x[l & 15].  Four exchange steps (partners l^8 by row_ror:8, l^7 by row_half_mirror, l^2
+// and l^1 by quad_perm); at each a lane keeps the half of its values selected by one
+// bit of its index and adds the partner's copy of that half.  Fixed order, no LDS.
+__device__ __forceinline__ double rs16(const double (&x)[16]) {
+    const int l = threadIdx.x & 15;
+    const bool b3 = l & 8, b2 = l & 4, b1 = l & 2, b0 = l & 1;
+    double y[8], z[4], w[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = (b3 ? x[8 + i] : x[i]) + dpp<0x128>(b3 ? x[i] : x[8 + i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = (b2 ? y[4 + i] : y[i]) + dpp<0x141>(b2 ? y[i] : y[4 + i]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) w[i] = (b1 ? z[2 + i] : z[i]) + dpp<0x4E>(b1 ? z[i] : z[2 + i]);
+    return (b0 ? w[1] : w[0]) + dpp<0xB1>(b0 ? w[0] : w[1]);
+}
+
 // Accumulate CH per-thread values x[0..CH) over the block's 256 rows into
 // acc[base .. base+CH) (LDS).  Fixed order: lane (col*16+part) sums rows q*16+part of
 // column col (q ascending), then a DPP row sum.
@@ -150,6 +167,23 @@ struct Row {
         }
         if (nc > MAXC) last = bld(tile, toff + cofs(nc - 1));
     }
+    // Same through a resource over the factor's whole basis (rows of two tiles in one
+    // wave): pairs past nc are skipped (wave-uniform), not range-checked.  Rows outside
+    // the basis pass toff >= 2^31, beyond the resource: every load returns zero.
+    // The caller sizes the row to the step (MAXC - 8 < nc <= MAXC, or MAXC == 8): only the
+    // last four pairs need the uniform column checks, and `last` is one of their columns.
+    __device__ __forceinline__ void loadm(rsrc_t basis, uint32_t toff, int nc) {
+        constexpr int P0 = MAXC / 2 - 4;
+        last = 0.0;
+#pragma unroll
+        for (int p = 0; p < MAXC / 2; ++p) {
+            d2_t x = (d2_t){0.0, 0.0};
+            if (p < P0 || 2 * p < nc) x = bld2(basis, toff + (uint32_t)p * (TPB * 16));
+            v[2 * p] = x.x;
+            v[2 * p + 1] = (p < P0 || 2 * p + 1 < nc) ? x.y : 0.0;
+            if (p >= P0) last = 2 * p == nc - 1 ? x.x : (2 * p + 1 == nc - 1 ? x.y : last);
+        }
+    }
 };
 
 // Store V[r, c] as a whole 16-byte column pair (`other` = the pair's other column): a lone
@@ -163,14 +197,70 @@ __device__ __forceinline__ void st_pair(double* V, int64_t tile_base, int c, int
 // wave-uniform addresses through the constant address space (scalar loads, many in
 // flight); otherwise h is an LDS copy (broadcast reads).  Entries past nc are finite
 // (zeroed at init or earlier coefficients) and meet R.v[c] == 0.
+// Two accumulators (even / odd columns, summed at the end) halve the dependent FMA chain;
+// the split depends on the column index only, so any register-row width gives the same
+// value (the zero columns past nc add exact zeros).
 template <int MAXC, bool SCALAR>
 __device__ __forceinline__ double row_dot(const Row<MAXC>& R, rsrc_t tile, uint32_t toff, int nc,
                                           const double* __restrict__ h) {
-    double s = 0.0;
+    double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) s += R.v[c] * (SCALAR ? CP4(h)[c] : h[c]);
-    for (int c = MAXC; c < nc; ++c) s += bld(tile, toff + cofs(c)) * (SCALAR ? CP4(h)[c] : h[c]);
-    return s;
+    for (int c = 0; c < MAXC; c += 2) {
+        s0 += R.v[c] * (SCALAR ? CP4(h)[c] : h[c]);
+        s1 += R.v[c + 1] * (SCALAR ? CP4(h)[c + 1] : h[c + 1]);
+    }
+    for (int c = MAXC; c < nc; ++c) {
+        const double x = bld(tile, toff + cofs(c)) * (SCALAR ? CP4(h)[c] : h[c]);
+        if (c & 1) s1 += x;
+        else s0 += x;
+    }
+    return s0 + s1;
+}
+// Two row dots at once (four independent chains), each bitwise equal to row_dot.
+template <int MAXC>
+__device__ __forceinline__ void row_dot2(const Row<MAXC>& R, const double* __restrict__ h,
+                                         const double* __restrict__ g, double& sh, double& sg) {
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    uint64_t ph = (uint64_t)h, pg = (uint64_t)g;
+#pragma unroll
+    for (int c0 = 0; c0 < MAXC; c0 += 8) {
+        // the next 8 coefficients of each vector are loaded (scalar) only after the
+        // previous ones were used: bounded SGPR live range, no spills
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+s"(ph), "+s"(pg) : "v"(a0), "v"(b0));
+        const double* hh = (const double*)ph;
+        const double* gg = (const double*)pg;
+#pragma unroll
+        for (int c = c0; c < c0 + 8; c += 2) {
+            a0 += R.v[c] * CP4(hh)[c];
+            a1 += R.v[c + 1] * CP4(hh)[c + 1];
+            b0 += R.v[c] * CP4(gg)[c];
+            b1 += R.v[c + 1] * CP4(gg)[c + 1];
+        }
+    }
+    sh = a0 + a1;
+    sg = b0 + b1;
+}
+// Same with both coefficient vectors staged in LDS (broadcast ds_read_b128), same order.
+template <int MAXC>
+__device__ __forceinline__ void row_dot2_lds(const Row<MAXC>& R, const double* __restrict__ h,
+                                             const double* __restrict__ g, double& sh, double& sg) {
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+#pragma unroll
+    for (int c0 = 0; c0 < MAXC; c0 += 8) {
+        __builtin_amdgcn_sched_barrier(0);   // coefficient reads in groups of 8 (register pressure)
+#pragma unroll
+        for (int c = c0; c < c0 + 8; c += 2) {
+            const d2_t hv = *(const d2_t*)(h + c);
+            const d2_t gv = *(const d2_t*)(g + c);
+            a0 += R.v[c] * hv.x;
+            a1 += R.v[c + 1] * hv.y;
+            b0 += R.v[c] * gv.x;
+            b1 += R.v[c + 1] * gv.y;
+        }
+    }
+    sh = a0 + a1;
+    sg = b0 + b1;
 }
 
 // Block-reduce V[r,i]*y for i < lim (lim == the row's loaded column count, so R.v[i]
@@ -197,7 +287,7 @@ __device__ __forceinline__ void reduce_row(const Row<MAXC>& R, rsrc_t tile, uint
 #pragma unroll
         for (int q = 0; q < CH; q += 2) {
             const d2_t p = bld2(tile, toff + cofs(c0 + q));
-            x[q] = p.x * y;
+            x[q] = (c0 + q < lim ? p.x : 0.0) * y;
             x[q + 1] = (c0 + q + 1 < lim ? p.y : 0.0) * y;
         }
         chunk_reduce(x, tr, acc, base + c0, first);
@@ -455,7 +545,8 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2(const DFac* __r
     store_partials(acc, d.P2, a.npart, gram ? 2 * nc + 2 : nc + 2);
 }
 
-// Write the pending column j+1 with no following step:
+// Write the pending column j+1 with no following step (U or W per a.ubuf: W after an
+// even one-sweep step):
 //   v = (U - V[:,0..j] h2) * inv_beta;  P1 = [ gram <V[:,c],v> (c<=j), <v,v>, <v,b> ]
 template <int MAXC>
 __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFac* __restrict__ F, KArgs a) {
@@ -475,7 +566,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
         const rsrc_t tv = mkrsrc(Vt, vrange(nc));
         Row<MAXC> R;
         R.load(tv, toff, nc);
-        const double up = ld(d.U, r);
+        const double up = ld(a.ubuf ? d.W : d.U, r);
         const double v = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, nc, h2)) * inv_beta : 0.0;
         st_pair(d.V, (int64_t)tile * TS, j + 1, threadIdx.x, v, ((j + 1) & 1) ? R.last : 0.0);
         reduce_row<MAXC>(R, tv, toff, nc, v, tr, acc, 0, first);
@@ -483,6 +574,206 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
         reduce_scalars<2>(e, tr, acc, nc, first);
     }
     store_partials(acc, d.P1, a.npart, nc + 2);
+}
+
+// ------------------------------------------------------------------ Arnoldi, one sweep per step
+// CGS2 with the reorthogonalization delayed by one step: step j
+// streams V[:, 0..j) ONCE.  Entering step j the device holds the raw vector u_j (once
+// orthogonalized, in U or W), its reorthogonalization coefficients c = h2[0..j) and
+// inv_beta, and h1 = g[0..j] (projection of A v_j on V[:, 0..j]).  Per row:
+//   v_j     = (u_j - V[:,0..j) c) * inv_beta                      -> V[:, j]
+//   u_{j+1} = A v_j - V[:,0..j) h1[0..j) - h1[j] v_j               -> the other buffer
+//   z       = A u_{j+1}
+//   P1 = [ <V[:,c],u> (c<j) | <V[:,c],z> (c<j) | <v_j,u>, <v_j,z>, <u,u>, <u,z>, <v_j,b>,
+//          <v_j,v_j> | gram <V[:,c],v_j> (c<j) ]
+// Both SpMVs read their vector from LDS, so each block works on an overlapping window of
+// 256 rows and owns the middle 256 - 2(hl+hu) of them: v_j is valid on the whole window,
+// u on all but hl/hu rows at its edges, z on all but 2hl/2hu -- the owned rows.  Halo rows
+// are recomputed from the same data in the same order as by their owner, so every block
+// sees bitwise the owner's values.  Only banded storage (hl, hu <= 4) takes this path.
+__device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= TPB ? TPB - 1 : (int)i); }
+
+// occupancy by register-row width (measured at C2: 4 waves/SIMD up to 32 columns, 3 up
+// to 56; 40 columns at 4 waves spill)
+#ifndef TK_D1_L4
+#define TK_D1_L4 32
+#endif
+#ifndef TK_D1_L3
+#define TK_D1_L3 56
+#endif
+// coefficients through the scalar cache (0) or staged in LDS (1: measured slower, VGPR spills)
+#ifndef TK_D1_COEF_LDS
+#define TK_D1_COEF_LDS 0
+#endif
+// Column dots: per window each 16-lane row of a wave reduce-scatters its products (rs16)
+// and every lane adds its result into a private LDS slot -- no barrier; the slots are
+// combined once, after the last window.  Chunk k < NUZ holds columns 8k..8k+7 times
+// (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row (16 columns
+// each).  acc[chunk][256]: slot t = (16-row group p = t >> 4, value s = t & 15).
+template <int MAXC, int FMT>
+__global__ __launch_bounds__(TPB) OCC_ATTR(TK_D1_L4, TK_D1_L3) void k_arn_d1(const DFac* __restrict__ F, KArgs a) {
+    constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
+    __shared__ double xs[4][TPB];   // v_j, u by window parity
+#if TK_D1_COEF_LDS
+    __shared__ __attribute__((aligned(16))) double cl[2][MAXC];   // c, h1
+#endif
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const DFac& d = F[blockIdx.y];
+#if TK_D1_ONEWIN
+    // XCD-aware slot: workgroups are dispatched round-robin over the 8 XCDs, so block x runs
+    // on XCD x % 8 (gridDim.x is a multiple of 8); each XCD takes a contiguous range of
+    // windows -- neighbouring windows share halo rows in its L2 and its partial stores
+    // fill whole lines there
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= d.nwin) return;
+#else
+    if ((int)blockIdx.x >= d.npd) return;
+    const int slot = blockIdx.x;
+#endif
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    double* acc = lds;
+    const int j = a.j, t = threadIdx.x;
+    const int hl = d.hl, hu = d.hu, WS = TPB - 2 * (hl + hu);
+    const double* Uin = a.ubuf ? d.W : d.U;
+    double* Uout = a.ubuf ? d.U : d.W;
+    const double inv_beta = ld(d.sc, SC_INVBETA);
+    const double* c = d.h2;
+    const double* h1 = d.g;
+    const double h1j = ld(d.g, j);
+    const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
+    const bool gram = d.track_gram != 0;
+    const int nch = NUZ + 1 + (gram ? NG : 0);
+    for (int k = 0; k < nch; ++k) acc[k * TPB + t] = 0.0;   // private slots
+#if TK_D1_COEF_LDS
+    // coefficient entries past the live ones are zero (init) and meet zero or finite
+    // basis entries
+    if (t < MAXC) {
+        cl[0][t] = ld(c, t);
+        cl[1][t] = ld(h1, t);
+    }
+    __syncthreads();
+#endif
+    int par = 0;
+#if TK_D1_ONEWIN
+    // one window per block (no window loop: nothing loop-invariant to hoist)
+    {
+        const int w = slot;
+#else
+    for (int w = blockIdx.x; w < d.nwin; w += d.npd, par ^= 1) {
+#endif
+        const int64_t S = (int64_t)w * WS - 2 * hl;
+        const int64_t r = S + t;
+        const bool inb = r >= 0 && r < a.ld;
+        const bool ok = r >= 0 && r < a.n;
+        const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * 16) : 0x80000000u;
+        Row<MAXC> R;
+        int jl = j;   // the per-pair conditions are re-derived each window (hoisted: SGPR spills)
+        asm volatile("" : "+s"(jl));
+        R.loadm(tv, toff, jl);
+        const double up = inb ? ld(Uin, r) : 0.0;
+        double sc, sh;
+#if TK_D1_COEF_LDS
+        row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sh);
+#else
+        row_dot2<MAXC>(R, c, h1, sc, sh);
+#endif
+        const double vj = ok ? (up - sc) * inv_beta : 0.0;
+        double* xv = xs[par];
+        double* xu = xs[2 + par];
+        xv[t] = vj;
+        __syncthreads();
+        const double av = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
+        const double u = ok ? av - (sh + h1j * vj) : 0.0;
+        xu[t] = u;
+        __syncthreads();
+        const double z = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xu[clamp_row(cc - S)]; }) : 0.0;
+        const bool own = ok && t >= 2 * hl && t < TPB - 2 * hu;
+        if (own) {
+            st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, (j & 1) ? R.last : 0.0);
+            st(Uout, r, u);
+        }
+        const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
+        const double bv = own ? ld(d.b, r) : 0.0;
+#ifndef TK_D1_NORED   // (timing experiment: column dots skipped)
+#pragma unroll
+        for (int k = 0; k < NUZ; ++k) {
+            if (8 * k < j) {
+                double x[16];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    x[2 * i] = R.v[8 * k + i] * uo;
+                    x[2 * i + 1] = R.v[8 * k + i] * zo;
+                }
+                acc[k * TPB + t] += rs16(x);
+            }
+        }
+        if (gram) {
+#pragma unroll
+            for (int k = 0; k < NG; ++k) {
+                if (16 * k < j) {
+                    double x[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) x[i] = 16 * k + i < MAXC ? R.v[16 * k + i < MAXC ? 16 * k + i : 0] * vo : 0.0;
+                    acc[(NUZ + 1 + k) * TPB + t] += rs16(x);
+                }
+            }
+        }
+#endif
+        {
+            double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * bv, vo * vj};
+            acc[NUZ * TPB + t] += rs16(x);
+        }
+    }
+    // combine the 16 row-group partials of every value (fixed order) -> P1
+    //   [ p (c<j) | q (c<j) | p_j, q_j, |u|^2, <u,z>, bt_j, gram_jj | gram (c<j) ]
+    __syncthreads();
+    for (int e = t; e < nch * 16; e += TPB) {
+        const int k = e >> 4, sl = e & 15;
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) sum += acc[k * TPB + p * 16 + sl];
+        int vi = -1;
+        if (k < NUZ) {
+            const int col = 8 * k + (sl >> 1);
+            if (col < j) vi = (sl & 1) ? j + col : col;
+        } else if (k == NUZ) {
+            if (sl < 6) vi = 2 * j + sl;
+        } else {
+            const int col = 16 * (k - NUZ - 1) + sl;
+            if (col < j) vi = 2 * j + 6 + col;
+        }
+        if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
+    }
+}
+
+// Initialization for the one-sweep Arnoldi: V[:,0] = U = inv(norm(b)) .* b
+// (src/decompositions.jl:112-118) and the first projection of A v_0 (v_0 is known at
+// every row from b, so the SpMV needs no halo):
+//   P1 = [ <v0,b>, <v0,v0>, <v0, A v0> ]
+template <int FMT>
+__global__ __launch_bounds__(TPB) void k_init_bd(const DFac* __restrict__ F, KArgs a) {
+#pragma clang fp contract(off)
+    KERNEL_PROLOGUE
+    if ((int)blockIdx.x >= d.npd) return;
+    double* acc = lds;
+    const double inv = ld(d.sc, SC_INVB);
+    if (threadIdx.x < 3) acc[threadIdx.x] = 0.0;   // npd may exceed the tile count
+    __syncthreads();
+    bool first = false;
+    const int nt = (int)(a.ld / TPB);
+    for (int tile = blockIdx.x; tile < nt; tile += d.npd, first = false) {
+        const int64_t r = (int64_t)tile * TPB + threadIdx.x;
+        const bool ok = r < a.n;
+        const double bv = ld(d.b, r);
+        const double v0 = inv * bv;
+        const double* bg = d.b;
+        const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t cc) { return mul_rn(inv, ld(bg, cc)); }) : 0.0;
+        st_pair(d.V, (int64_t)tile * TS, 0, threadIdx.x, v0, 0.0);
+        st(d.U, r, v0);
+        const double e[3] = {v0 * bv, v0 * v0, v0 * av};
+        reduce_scalars<3>(e, tr, acc, 0, first);
+    }
+    store_partials(acc, d.P1, d.npd, 3);
 }
 
 // ------------------------------------------------------------------ Lanczos (TTR)
@@ -593,18 +884,20 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
     const int c = blockIdx.x;
     if (c >= nv) return;
     if (gate && ld(d.sc, SC_REDO) == 0.0) return;
+    if (npart <= 0) npart = d.npd;
     const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
     const int l = threadIdx.x;
-    double part[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int b = l + 64 * i;
-        part[i] = b < npart ? ld(P, b) : 0.0;
-    }
     double s = 0.0;
+    for (int b0 = 0; b0 < npart; b0 += 1024) {   // rounds of 16 independent loads per lane
+        double part[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) s += part[i];
-    for (int b = l + 1024; b < npart; b += 64) s += ld(P, b);
+        for (int i = 0; i < 16; ++i) {
+            const int b = b0 + l + 64 * i;
+            part[i] = b < npart ? ld(P, b) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += part[i];
+    }
     s = row16_sum(s);
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
@@ -698,10 +991,99 @@ __device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const doubl
     put_gram(rec, kmax, j, red2 + j + 3, red2[j + 2], d.track_gram);
 }
 
+// One-sweep Arnoldi post-processing of step j.  RED1 holds (k_arn_d1)
+//   p = <V[:,c],u> (c<j) | q = <V[:,c],z> (c<j) | p_j, q_j, |u|^2, <u,z>, bt_j, gram_jj | gram (c<j)
+// with u = u_{j+1}, z = A u.  The reorthogonalization coefficients of u are c = p; then
+//   H[0..j, j] = h1 + c,  beta = H[j+1, j] = sqrt(|u|^2 - |c|^2)        (CGS2 of
+//   src/orthogonal_bases.jl:22-36 in exact arithmetic),  v_{j+1} = (u - V c) * inv(beta),
+// and the first projection of A v_{j+1} = (z - V Hbar c) * inv(beta) (Arnoldi relation for
+// the small correction A V c) follows from the sweep's dots with V'V = I, V'v_{j+1} = 0:
+//   h1'[l] = (q_l - (Hbar c)_l) * inv(beta)   (l <= j)
+//   h1'[j+1] = ((<u,z> - c.q) * inv(beta) - (Hbar c)_{j+1}) * inv(beta)
+// c -> h2, h1' -> g (the next sweep's coefficients), inv(beta) -> scalars, the step's
+// record (H column j, beta, bt_j and the Gram row of column j).
+__device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* Hs, double* cs, double* qs,
+                           double* h1s, double* sh) {
+    const int j = a.j, kmax = a.kmax, KP = kmax + 2;
+    const int t = threadIdx.x;
+    const double* R = d.RED1;
+    double* Hc = d.H + (int64_t)j * KP;
+    const int J2 = j + 2;
+    for (int i = t; i <= j; i += TPB) {
+        cs[i] = i < j ? ld(R, i) : ld(R, 2 * j);
+        qs[i] = i < j ? ld(R, j + i) : ld(R, 2 * j + 1);
+        h1s[i] = ld(d.g, i);
+    }
+    __syncthreads();
+    double cc = 0.0, cq = 0.0;
+    for (int i = t; i <= j; i += TPB) {
+        const double hv = h1s[i] + cs[i];
+        st(Hc, i, hv);
+        st(d.h2, i, cs[i]);
+        st(rec, i, hv);
+        if (Hs) Hs[j * J2 + i] = hv;
+        cc += cs[i] * cs[i];
+        cq += cs[i] * qs[i];
+    }
+    if (Hs)
+        for (int idx = t; idx < j * J2; idx += TPB) {
+            const int i = idx / J2, l = idx - i * J2;
+            Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+        }
+    cc = row16_sum(cc);
+    cc += __shfl_xor(cc, 16);
+    cc += __shfl_xor(cc, 32);
+    cq = row16_sum(cq);
+    cq += __shfl_xor(cq, 16);
+    cq += __shfl_xor(cq, 32);
+    if ((t & 63) == 0) {
+        sh[t >> 6] = cc;
+        sh[4 + (t >> 6)] = cq;
+    }
+    __syncthreads();
+    if (t == 0) {
+        const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+        const double bsq = ld(R, 2 * j + 2) - s2;
+        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+        st(Hc, j + 1, beta);
+        if (Hs) Hs[j * J2 + j + 1] = beta;
+        st(rec, j + 1, beta);
+        st(rec, rec_beta(kmax), beta);
+        st(d.sc, SC_BETA, beta);
+        st(d.sc, SC_INVBETA, 1.0 / beta);
+        st(d.sc, SC_BETAPREV, beta);
+        sh[8] = beta;
+        sh[9] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
+    }
+    __syncthreads();
+    const double beta = sh[8], ib = 1.0 / beta;
+    for (int l = t; l <= j + 1; l += TPB) {
+        double s = 0.0;
+        for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) {
+            const double hv = Hs ? Hs[i * J2 + l]
+                                 : (i == j ? (l == j + 1 ? beta : ld(Hc, l)) : ld(d.H, (int64_t)i * KP + l));
+            s += hv * cs[i];
+        }
+        const double h = l <= j ? (qs[l] - s) * ib : ((ld(R, 2 * j + 3) - sh[9]) * ib - s) * ib;
+        st(d.g, l, h);
+    }
+    // Gram row of column j: [gram (c<j), gram_jj]
+    if (d.track_gram) {
+        for (int i = t; i <= j; i += TPB) st(rec, rec_gram(kmax) + i, i < j ? ld(R, 2 * j + 6 + i) : ld(R, 2 * j + 5));
+    }
+    if (t == 0) {
+        st(rec, rec_bt(kmax), ld(R, 2 * j + 4));
+        st(rec, rec_col(kmax), (double)j);
+        st(rec, rec_tracked(kmax), d.track_gram ? 1.0 : 0.0);
+    }
+}
+
 __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag,
                                               int clear) {
     __shared__ double sh[16];
     __shared__ double h2s[1024 + 8];
+    __shared__ double qs[1024 + 8];
+    __shared__ double h1s[1024 + 8];
     extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
     if (a.gate && ld(d.sc, SC_REDO) == 0.0) return;
@@ -730,11 +1112,22 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_INIT_B) {
         put_gram(rec, kmax, 0, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
         if (t == 0 && d.track_gram) st(d.lossrow, 0, loss_row(d.RED1 + 1, 0));
+        if (t == 0 && flag) {
+            // one-sweep Arnoldi: step 0 re-derives v_0 = U * 1.0 with no coefficients;
+            // h1 = [<v0, A v0>]
+            st(d.g, 0, ld(d.RED1, 2));
+            st(d.sc, SC_INVBETA, 1.0);
+        }
         return;
     }
     if (kind == POST_ARN) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // = launcher's size
         post_arn(d, a, rec, d.RED1, d.RED2, Hs, h2s, sh);
+        return;
+    }
+    if (kind == POST_ARN_D) {
+        double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;
+        post_arn_d(d, a, rec, Hs, h2s, qs, h1s, sh);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -954,6 +1347,29 @@ void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_arn_finalize<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
 }
+// the one-sweep kernels exist for banded storage only (the host routes other formats to CGS2)
+template <class F>
+static void with_band_fmt(int fmt, F f) {
+    if (fmt == SPM_DIAT) f(IC<SPM_DIAT>{});
+    else f(IC<SPM_DIA>{});
+}
+void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+    with_band_fmt(a.fmt, [&](auto FM) {
+        hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
+    });
+}
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+    // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks
+    const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
+    const size_t lds = (size_t)(M / 8 + 1 + (M + 15) / 16) * TPB * sizeof(double);
+    with_band_fmt(a.fmt, [&](auto FM) {
+        with_maxc(a.j, [&](auto M) {
+            hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value>),
+                               dim3(TK_D1_ONEWIN ? (npd + 7) / 8 * 8 : npd, nf), dim3(TPB),
+                               lds, s, F, a);
+        });
+    });
+}
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     const size_t lds = lds_bytes(1, a.kmax, 0);
     with_fmt(a.fmt, [&](auto FM) {
@@ -977,7 +1393,7 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
 }
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
-    const size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
+    const size_t lds = ((kind == POST_ARN || kind == POST_ARN_D) && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
     hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), lds, s, F, a, kind, flag, clear);
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,

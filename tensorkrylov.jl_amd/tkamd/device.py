@@ -125,6 +125,12 @@ class DeviceDecomposition:
         self.h = h
         self._mats = mats
 
+    @property
+    def arnoldi_sweeps(self):
+        """Sweeps over V per Arnoldi step (1: delayed-reorthogonalization CGS2 on banded
+        A_s, 2: CGS2), 0 for the Lanczos methods (tk_decomp_arnoldi_sweeps)."""
+        return int(self.ctx._lib.tk_decomp_arnoldi_sweeps(self.h))
+
     def _rec(self):
         return np.zeros((self.d_total, self.m))
 

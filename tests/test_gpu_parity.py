@@ -93,13 +93,20 @@ def test_spmv_one_based_julia_csc(ctx):
 
 
 # ------------------------------------------------------------------ per-factor steps
-def _run_device(ctx, method, csc, bs, K, track_all=True):
+def _run_device(ctx, method, csc, bs, K, track_all=True, sweeps=None, peek=None):
+    """init, K steps, flush; records and bases.  sweeps: expected arnoldi_sweeps of the
+    decomposition (asserted); peek: step after which the basis is read back mid-run (a
+    flush of the pending column, then the sweep continues)."""
     tk = _tk()
     A = tk.DeviceMatrix(ctx, csc)
     dev = tk.DeviceDecomposition(ctx, method, len(bs), 0, [A] * len(bs), bs, K, track_all_gram=track_all)
+    if sweeps is not None:
+        assert dev.arnoldi_sweeps == sweeps
     recs = [dev.init()]
     for j in range(K):
         recs.append(dev.step(j))
+        if peek is not None and j == peek:
+            dev.basis(0, 0, j + 2)
     recs.append(dev.flush())
     V = [dev.basis(f, 0, K + 1) for f in range(len(bs))]
     dev.close()
@@ -107,16 +114,37 @@ def _run_device(ctx, method, csc, bs, K, track_all=True):
     return recs, V
 
 
+def _orth_env(orth, monkeypatch):
+    """'auto': banded A_s take the one-sweep Arnoldi (delayed reorthogonalization),
+    'cgs2': TKHIP_ARNOLDI=cgs2 forces the two-sweep CGS2 for every storage."""
+    if orth == "cgs2":
+        monkeypatch.setenv("TKHIP_ARNOLDI", "cgs2")
+    else:
+        monkeypatch.delenv("TKHIP_ARNOLDI", raising=False)
+
+
+def _arnoldi_oracle(csc, b, K):
+    fo = O.Factor(csc, b, K)
+    for j in range(1, K + 1):
+        fo.arnoldi_mgs(j)
+    return fo
+
+
+@pytest.mark.parametrize("orth", ["auto", "cgs2"])
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 50), ("ConvDiff", 200, 50),
                                      ("Laplace", 1000, 40), ("RandSparseSPD", 3000, 30),
                                      ("Laplace", 1000, 80), ("ConvDiff", 300, 70), ("Laplace", 7, 5)])
-def test_arnoldi_matches_oracle(ctx, cls, n, K):
-    """Arnoldi (MGS2 in the reference, fused CGS2 here) per step vs the oracle, incl.
-    kmax > 64 (columns beyond the register row are streamed) and n < one tile."""
+def test_arnoldi_matches_oracle(ctx, cls, n, K, orth, monkeypatch):
+    """Arnoldi (MGS2 in the reference; one-sweep delayed-reorthogonalization CGS2 for the
+    banded gallery matrices, two-sweep CGS2 otherwise or when forced) per step vs the
+    oracle, incl. kmax > 64 (columns beyond the register row are streamed) and n < one
+    tile."""
     tk = _tk()
+    _orth_env(orth, monkeypatch)
     csc = tk.assemble_matrix(n, cls)
     bs = _rhs(n, 2, 7, distinct=True)
-    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K)
+    sweeps = 1 if (orth == "auto" and cls != "RandSparseSPD") else 2
+    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, sweeps=sweeps)
     lay = tk._lib.RecordLayout(K)
     for f, b in enumerate(bs):
         fo = O.Factor(csc, b, K)
@@ -143,24 +171,55 @@ def test_arnoldi_matches_oracle(ctx, cls, n, K):
         assert np.abs(np.tril(G) - Gref).max() <= 1e-13
 
 
-def test_arnoldi_general_band_matches_oracle(ctx):
-    """Arnoldi over a non-Toeplitz band (the DIA path that streams matrix values)."""
+def _band(n, offs, seed):
+    rng = np.random.default_rng(seed)
+    A = np.zeros((n, n))
+    for o in offs:
+        idx = np.arange(max(0, -o), min(n, n - o))
+        A[idx, idx + o] = -rng.random(len(idx)) if o else 4.0 + len(offs) + rng.random(len(idx))
+    return A
+
+
+@pytest.mark.parametrize("orth", ["auto", "cgs2"])
+@pytest.mark.parametrize("n,offs,K", [(900, (-1, 0, 1), 30), (777, (-2, 0, 3), 25), (1010, (-4, 0, 4), 20),
+                                      (600, (-1, 0, 1, 2), 30), (756, (-1, 0, 1), 12), (250, (-2, -1, 0, 1), 40),
+                                      (3, (-1, 0, 1), 2)])
+def test_arnoldi_general_band_matches_oracle(ctx, n, offs, K, orth, monkeypatch):
+    """Arnoldi over non-Toeplitz bands (the DIA path that streams matrix values) with
+    lower/upper bandwidths up to 4: the one-sweep kernel's overlapping windows (halo rows
+    recomputed by both neighbours), n at and around window-stride multiples, n < window."""
     tk = _tk()
-    n, K = 900, 30
-    rng = np.random.default_rng(9)
-    A = np.diag(4.0 + rng.random(n)) + np.diag(-rng.random(n - 1), 1) + np.diag(-rng.random(n - 1), -1)
-    csc = O.dense_to_csc(A)
+    _orth_env(orth, monkeypatch)
+    csc = O.dense_to_csc(_band(n, offs, 9))
     bs = _rhs(n, 2, 4, distinct=True)
-    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K)
+    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, sweeps=1 if orth == "auto" else 2)
     for f, b in enumerate(bs):
-        fo = O.Factor(csc, b, K)
-        for j in range(1, K + 1):
-            fo.arnoldi_mgs(j)
+        fo = _arnoldi_oracle(csc, b, K)
         Hd = np.zeros((K + 1, K))
         for j in range(K):
             Hd[:j + 2, j] = recs[j + 1][f, :j + 2]
         assert np.abs(Hd - fo.H[:K + 1, :K]).max() <= 1e-12 * np.abs(fo.H).max()
         assert np.abs(V[f] - fo.V[:, :K + 1]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("cls", ["Laplace", "RandSparseSPD"])
+def test_arnoldi_mid_run_flush(ctx, cls):
+    """Reading the basis mid-run flushes the pending column, then the sweep continues.
+    One-sweep (banded): the next step re-derives the flushed column from the same
+    operands, so every record and the final basis are bitwise those of the uninterrupted
+    run.  CGS2 (SELL storage): the next step applies A to the stored column instead of
+    the Arnoldi relation -- equal to rounding (1e-12 relative)."""
+    tk = _tk()
+    n, K = 2000, 24
+    csc = tk.assemble_matrix(n, cls)
+    bs = _rhs(n, 2, 21, distinct=True)
+    ra, Va = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K)
+    rb, Vb = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, peek=9)
+    exact = cls == "Laplace"
+    for x, y in zip(ra[:-1], rb[:-1]):
+        assert np.array_equal(x, y) if exact else np.allclose(x, y, rtol=1e-12, atol=1e-12 * np.abs(x).max())
+    for x, y in zip(Va, Vb):
+        assert np.array_equal(x, y) if exact else np.abs(x - y).max() <= 1e-12
 
 
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20)])
