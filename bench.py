@@ -178,7 +178,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     host_us_per_step = 1e6 * host_issue[0] / max(host_issue[1], 1) / K
-    step_ms, step_cnt = ctx.timing_read(L.T_STEP)
+    sweep_ms, sweep_cnt = ctx.timing_read(L.T_SWEEP)    # K step groups per sweep
+    step_ms, step_cnt = sweep_ms, sweep_cnt * K
     vy_ms, vy_cnt = ctx.timing_read(L.T_VY)
     if world > 1:                               # max over ranks (one-hot sum)
         v = np.zeros(world)

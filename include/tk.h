@@ -174,9 +174,11 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
 tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X);
 
 /* ---------------------------------------------------------------- timing hooks */
-/* Average device time (ms) per launch of the named kernel class recorded with HIP
- * events on the ctx stream since the last reset; classes: 0 = all step kernels,
- * 1 = the dominant streaming kernel (Arnoldi/Lanczos projection), 2 = basis_mul. */
+/* Device time (ms, total) and launch count of a kernel class recorded with HIP events on
+ * the ctx stream since the last tk_timing_enable.  on = 1: classes 0 (one step group per
+ * tk_decomp_step called outside a sweep), 5 (basis_mul), 6 (exchange) and 7 (one
+ * tk_decomp_sweep: its step groups back to back); on = 2 adds per-kernel classes
+ * 1 (first / one-sweep pass), 2 (second pass), 3 (finalize), 4 (reduce + post). */
 tk_status tk_timing_enable(tk_ctx* ctx, int on);
 tk_status tk_timing_read(tk_ctx* ctx, int cls, double* total_ms, long* launches);
 

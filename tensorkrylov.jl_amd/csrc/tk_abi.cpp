@@ -54,7 +54,8 @@ static tk_status fail(int code, const char* fmt, ...) {
     } while (0)
 
 // ------------------------------------------------------------------ context
-enum { TCLS_STEP = 0, TCLS_PASS1 = 1, TCLS_PASS2 = 2, TCLS_FIN = 3, TCLS_RED = 4, TCLS_VY = 5, TCLS_XCH = 6, TCLS_N = 8 };
+enum { TCLS_STEP = 0, TCLS_PASS1 = 1, TCLS_PASS2 = 2, TCLS_FIN = 3, TCLS_RED = 4, TCLS_VY = 5, TCLS_XCH = 6,
+       TCLS_SWEEP = 7, TCLS_N = 8 };
 
 struct tk_ctx {
     int device = 0;
@@ -94,7 +95,9 @@ struct Timer {
             c->evpool.pop_back();
             return true;
         }
-        return hipEventCreate(&e) == hipSuccess;
+        // timing only: no system-scope fence on record (with it every record cost ~10 us of
+        // GPU idle time -- a cache writeback -- between the kernels it brackets)
+        return hipEventCreateWithFlags(&e, hipEventDisableSystemFence) == hipSuccess;
     }
     ~Timer() {
         if (!on) return;
@@ -527,6 +530,7 @@ struct tk_decomp {
     int npd = 0;            // max DFac::npd over the local factors (grid width of k_arn_d1)
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
+    bool in_sweep = false;  // inside tk_decomp_sweep: one timing pair for the whole sweep
     int last_j = -1;
     std::vector<tk_mat*> mats;
     std::vector<DFac> hf;   // host copy of descriptors
@@ -680,8 +684,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->ev_c.assign(kmax + 2, nullptr);
         dc->ev_x.assign(kmax + 2, nullptr);
         for (int i = 0; i < kmax + 2; ++i) {
-            hipError_t e = hipEventCreateWithFlags(&dc->ev_c[i], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&dc->ev_x[i], hipEventDisableTiming);
+            // stream-order events between the compute and exchange streams of this device:
+            // kernel completion already releases at device scope; no system-scope fence
+            const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
+            hipError_t e = hipEventCreateWithFlags(&dc->ev_c[i], fl);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&dc->ev_x[i], fl);
             if (e != hipSuccess) {
                 free_decomp(dc);
                 return fail(TK_ERR_HIP, "hipEventCreate: %s", hipGetErrorString(e));
@@ -715,7 +722,9 @@ tk_status tk_decomp_destroy(tk_decomp* dc) {
 // Before a slot's send rows are rewritten, the previous all-reduce of that slot must
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
-    if (dc->recv != dc->rec) HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[slot], 0));
+    // (an already completed exchange needs no wait packet in the compute queue)
+    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[slot]) != hipSuccess)
+        HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[slot], 0));
     return TK_OK;
 }
 
@@ -833,7 +842,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_status st = slot_guard(dc, slot);
     if (st) return st;
     KArgs a = base_args(dc, j, slot);
-    Timer step_timer(c, TCLS_STEP, 1);
+    Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
     if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
         // overwritten by the CGS2 step below, which reports column j again)
@@ -918,11 +927,14 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
 
 tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
     CHECKARG(dc, "NULL decomp");
-    for (int j = j0; j < j1; ++j) {
-        tk_status st = tk_decomp_step(dc, j, nullptr);
-        if (st) return st;
-    }
-    return TK_OK;
+    // one event pair brackets the whole sweep (events between the steps would idle the
+    // GPU for their fences and inflate the very time they measure)
+    Timer sweep_timer(dc->ctx, TCLS_SWEEP, 1);
+    dc->in_sweep = true;
+    tk_status st = TK_OK;
+    for (int j = j0; j < j1 && st == TK_OK; ++j) st = tk_decomp_step(dc, j, nullptr);
+    dc->in_sweep = false;
+    return st;
 }
 
 tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {

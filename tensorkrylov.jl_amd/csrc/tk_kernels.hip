@@ -611,7 +611,16 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 // (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row (16 columns
 // each).  acc[chunk][256]: slot t = (16-row group p = t >> 4, value s = t & 15).
 template <int MAXC, int FMT>
-__global__ __launch_bounds__(TPB) OCC_ATTR(TK_D1_L4, TK_D1_L3) void k_arn_d1(const DFac* __restrict__ F, KArgs a) {
+#ifndef TK_D1_OCCT
+#define TK_D1_OCCT 1
+#endif
+#if TK_D1_OCCT
+// narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
+#define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
+#else
+#define D1_OCC OCC_WAVES(TK_D1_L4, TK_D1_L3)
+#endif
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
     __shared__ double xs[4][TPB];   // v_j, u by window parity
 #if TK_D1_COEF_LDS
@@ -904,6 +913,39 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
     if (l == 0) st(which == 1 ? d.RED1 : d.RED2, c, s);
 }
 
+// Same for the one-sweep kernel's per-window partials (npart = DFac::npd, ~4k at n = 2^20):
+// four waves per value, each lane a strided subset in rounds of 16 independent loads, DPP
+// row sums, the 16 row totals summed in fixed order.
+__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv) {
+    __shared__ double rs[16];
+    const DFac& d = F[blockIdx.y];
+    const int c = blockIdx.x;
+    if (c >= nv) return;
+    const int npart = d.npd;
+    const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
+    const int t = threadIdx.x;
+    double s = 0.0;
+    for (int b0 = 0; b0 < npart; b0 += 4096) {
+        double part[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int b = b0 + t + 256 * i;
+            part[i] = b < npart ? ld(P, b) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += part[i];
+    }
+    s = row16_sum(s);
+    if ((t & 15) == 0) rs[t >> 4] = s;
+    __syncthreads();
+    if (t == 0) {
+        double r = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) r += rs[q];
+        st(which == 1 ? d.RED1 : d.RED2, c, r);
+    }
+}
+
 // ------------------------------------------------------------------ post-processing
 // One 256-thread block per local factor: reduced values -> H / beta / records.
 // `clear` zeroes the factor's record row first (the first post of a record slot).
@@ -954,10 +996,18 @@ __device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const doubl
         if (Hs) Hs[j * J2 + i] = hv;
         hh += h2 * h2;
     }
-    if (Hs)
-        for (int idx = t; idx < j * J2; idx += TPB) {
-            const int i = idx / J2, l = idx - i * J2;
-            Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+    if (Hs)   // stage Hbar[:, 0..j): eight independent loads in flight per thread
+        for (int i0 = 0; i0 < j * J2; i0 += 8 * TPB) {
+            double hv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int idx = i0 + q * TPB + t;
+                const int i = idx / J2, l = idx - i * J2;
+                hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
         }
     hh = row16_sum(hh);
     hh += __shfl_xor(hh, 16);
@@ -1025,10 +1075,18 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
         cc += cs[i] * cs[i];
         cq += cs[i] * qs[i];
     }
-    if (Hs)
-        for (int idx = t; idx < j * J2; idx += TPB) {
-            const int i = idx / J2, l = idx - i * J2;
-            Hs[idx] = l <= i + 1 ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+    if (Hs)   // stage Hbar[:, 0..j): eight independent loads in flight per thread
+        for (int i0 = 0; i0 < j * J2; i0 += 8 * TPB) {
+            double hv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int idx = i0 + q * TPB + t;
+                const int i = idx / J2, l = idx - i * J2;
+                hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
         }
     cc = row16_sum(cc);
     cc += __shfl_xor(cc, 16);
@@ -1389,7 +1447,10 @@ void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate) {
-    hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
+    if (npart <= 0 && !gate)
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv);
+    else
+        hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("TKHIP_LIB", os.path.join(_HERE, "libtkhip.so"))
 TK_ARNOLDI, TK_LANCZOS, TK_LANCZOS_REORTH = 0, 1, 2
 
 # timing classes (tk_abi.cpp TCLS_*)
-T_STEP, T_PASS1, T_PASS2, T_FIN, T_RED, T_VY, T_XCH = 0, 1, 2, 3, 4, 5, 6
+T_STEP, T_PASS1, T_PASS2, T_FIN, T_RED, T_VY, T_XCH, T_SWEEP = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 class TKError(RuntimeError):
