@@ -238,6 +238,9 @@ def main():
                    for k in range(1, K + 1)) * part.nf
     step_avg_s = (step_ms / 1e3) / max(step_cnt, 1)
     achieved = (alg_step / K) / step_avg_s / 1e9 if step_cnt else None
+    # the same steps priced in the reference algorithm's bytes (MGS2 streams V
+    # twice per step): what a two-sweep implementation would have to move at this rate
+    ref_step = sum(alg_bytes_step(n, nnz, k, method, 2) for k in range(1, K + 1)) * part.nf
     vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
     vy_flops = 2 * n * K * t_rank * part.nf
     vy_s = (vy_ms / 1e3) / max(vy_cnt, 1)
@@ -291,6 +294,9 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg_step / K,
                 "arnoldi_sweeps_over_V": sweeps if method == "TensorArnoldi" else None,
+                **({"reference_algorithm_bytes_per_launch": ref_step / K,
+                    "reference_algorithm_effective_GBs": round((ref_step / K) / step_avg_s / 1e9, 1)}
+                   if method == "TensorArnoldi" and sweeps == 1 and step_cnt else {}),
                 "avg_launch_us": round(step_avg_s * 1e6, 2),
             },
             "host_issue_us_per_iteration": round(host_us_per_step, 2),
