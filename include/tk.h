@@ -123,6 +123,11 @@ tk_status tk_decomp_destroy(tk_decomp* dc);
  * Lanczos methods. */
 int tk_decomp_arnoldi_sweeps(tk_decomp* dc);
 
+/* 1 when the records exchange of this handle is triggered by a signal word the step's last
+ * kernel increments (hipStreamWaitValue64 on the exchange stream), 0 when it uses an event
+ * per step or there is no exchange (single rank; TK_LANCZOS_REORTH; TKHIP_XCH_EVENTS=1). */
+int tk_decomp_exchange_signalled(tk_decomp* dc);
+
 /* Per-factor record layout (doubles; m = tk_record_len(kmax)), written by every step:
  *   [0 .. kmax+1]        H[0..j+1, j] as computed by this step (rest 0)
  *   [kmax+2 .. 2kmax+3]  Gram row G[c, 0..c] = V[:,c]' V[:,0..c] of column c below

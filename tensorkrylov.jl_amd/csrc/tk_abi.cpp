@@ -531,6 +531,10 @@ struct tk_decomp {
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
     bool in_sweep = false;  // inside tk_decomp_sweep: one timing pair for the whole sweep
+    // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
+    // exchange stream waits (hipStreamWaitValue64) for xcount
+    unsigned long long* xflag = nullptr;
+    unsigned long long xcount = 0;
     int last_j = -1;
     std::vector<tk_mat*> mats;
     std::vector<DFac> hf;   // host copy of descriptors
@@ -564,6 +568,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->scratch) hipFree(dc->scratch);
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
+    if (dc->xflag) hipFree(dc->xflag);
     delete dc;
 }
 
@@ -695,11 +700,32 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
     }
+    if (dc->recv != dc->rec && method != TK_LANCZOS_REORTH) {
+        int ok = 0;
+        const char* e = getenv("TKHIP_XCH_EVENTS");
+        if (!(e && e[0] == '1') &&
+            hipDeviceGetAttribute(&ok, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && ok) {
+            void* p = nullptr;
+            if (hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p) {
+                // the count starts wherever the word is (no memset on signal memory)
+                unsigned long long v0 = 0;
+                if (hipMemcpy(&v0, p, 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                    dc->xflag = (unsigned long long*)p;
+                    dc->xcount = v0;
+                } else {
+                    hipFree(p);
+                }
+            }
+        }
+        (void)hipGetLastError();   // an unsupported signal path must not leave a sticky error
+    }
     c->refs++;
     for (tk_mat* A : dc->mats) A->refs++;
     *out = dc;
     return TK_OK;
 }
+
+int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
 
 int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
     if (!dc || dc->method != TK_ARNOLDI) return 0;
@@ -741,21 +767,28 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.fmt = dc->fmt;
     a.gate = 0;
     a.ubuf = 0;
+    a.xflag = nullptr;
     return a;
 }
 
 // One RCCL all-reduce per record slot: the send buffer holds only this rank's rows
 // (other rows stay zero forever), so the sum is exact and every rank receives every
 // factor's record.
-static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out) {
+static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out, bool signalled = false) {
     tk_ctx* c = dc->ctx;
     const size_t cnt = (size_t)dc->d_total * dc->m;
     double* s = dc->rec + (size_t)slot * cnt;
     double* r = dc->recv + (size_t)slot * cnt;
     if (dc->recv != dc->rec) {
-        // the exchange runs on its own stream, overlapping the next step's kernels
-        HIPCHK(hipEventRecord(dc->ev_c[slot], c->stream));
-        HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[slot], 0));
+        // the exchange runs on its own stream, overlapping the next step's kernels; it
+        // starts when the step's k_post blocks have signalled (or after an event marker)
+        if (signalled) {
+            HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcount, hipStreamWaitValueGte,
+                                        0xFFFFFFFFFFFFFFFFull));
+        } else {
+            HIPCHK(hipEventRecord(dc->ev_c[slot], c->stream));
+            HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[slot], 0));
+        }
         {
             Timer tm(c, TCLS_XCH, 2, c->xstream);
             NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->xstream));
@@ -842,6 +875,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_status st = slot_guard(dc, slot);
     if (st) return st;
     KArgs a = base_args(dc, j, slot);
+    KArgs ax = a;          // the step's last k_post signals the exchange stream
+    ax.xflag = dc->xflag;
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
     if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
@@ -857,7 +892,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         a.ubuf = j & 1;
         RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, dc->npd, s), "arn_d1");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_D, 0, 1, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN_D, 0, 1, s), "post");
         dc->pending = true;
     } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
@@ -869,7 +904,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
         RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN, fused ? 1 : 0, 1, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;
@@ -882,7 +917,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         }
         RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, fused ? 1 : 0, 1, s), "post");
+        RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_LAN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;
     } else {
         // TensorLanczosReorth (src/orthogonal_bases.jl:98-139): TTR, write v_{j+1} with its
@@ -920,9 +955,11 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
     if (j != dc->jnext) return fail(TK_ERR_STATE, "step %d requested, next step is %d", j, dc->jnext);
     if (j >= dc->kmax) return fail(TK_ERR_ARG, "step %d >= kmax %d", j, dc->kmax);
     HIPCHK(hipSetDevice(dc->ctx->device));
+    const bool sig = dc->xflag != nullptr;
+    if (sig) dc->xcount += (unsigned long long)dc->nf;   // the step's k_post adds one per factor
     tk_status st = step_impl(dc, j, rec_out);
     if (st) return st;
-    return exchange_and_copy(dc, j + 1, rec_out);
+    return exchange_and_copy(dc, j + 1, rec_out, sig);
 }
 
 tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {

@@ -78,6 +78,8 @@ struct KArgs {
     int fmt;          // storage common to all factors of the launch: 1 DIA, 2 SELL, 3 CSR, 0 mixed
     int gate;         // 1: a block does nothing unless its factor's SC_REDO flag is set
     int ubuf;         // one-sweep Arnoldi: 0 = the pending raw vector u is in U, 1 = in W
+    unsigned long long* xflag;   // non-null: each k_post block adds 1 once its record is
+                                 // written (signal memory the exchange stream waits on)
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register

@@ -925,15 +925,15 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
     const int t = threadIdx.x;
     double s = 0.0;
-    for (int b0 = 0; b0 < npart; b0 += 4096) {
-        double part[16];
+    for (int b0 = 0; b0 < npart; b0 += 6144) {   // one round up to 6144 partials (n ~ 1.5M)
+        double part[24];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < 24; ++i) {
             const int b = b0 + t + 256 * i;
             part[i] = b < npart ? ld(P, b) : 0.0;
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s += part[i];
+        for (int i = 0; i < 24; ++i) s += part[i];
     }
     s = row16_sum(s);
     if ((t & 15) == 0) rs[t >> 4] = s;
@@ -1059,6 +1059,21 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
     const double* R = d.RED1;
     double* Hc = d.H + (int64_t)j * KP;
     const int J2 = j + 2;
+    // every global load of the kernel in one round trip: Hbar[:, 0..j) (16 per thread in
+    // flight; a loop beyond j = 62), the reduced dots and the current h1
+    if (Hs)
+        for (int i0 = 0; i0 < j * J2; i0 += 16 * TPB) {
+            double hv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int idx = i0 + q * TPB + t;
+                const int i = idx / J2, l = idx - i * J2;
+                hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * KP + l) : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
+        }
     for (int i = t; i <= j; i += TPB) {
         cs[i] = i < j ? ld(R, i) : ld(R, 2 * j);
         qs[i] = i < j ? ld(R, j + i) : ld(R, 2 * j + 1);
@@ -1075,19 +1090,6 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
         cc += cs[i] * cs[i];
         cq += cs[i] * qs[i];
     }
-    if (Hs)   // stage Hbar[:, 0..j): eight independent loads in flight per thread
-        for (int i0 = 0; i0 < j * J2; i0 += 8 * TPB) {
-            double hv[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int idx = i0 + q * TPB + t;
-                const int i = idx / J2, l = idx - i * J2;
-                hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * KP + l) : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
-        }
     cc = row16_sum(cc);
     cc += __shfl_xor(cc, 16);
     cc += __shfl_xor(cc, 32);
@@ -1136,6 +1138,19 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
     }
 }
 
+// Tell the exchange stream that this block's record row is complete: all threads' stores
+// are ordered before thread 0's device-scope release, then one system-scope add to the
+// signal word (the stream waits for the count of all of the step's blocks; no event marker
+// in the compute queue).
+__device__ __forceinline__ void post_signal(const KArgs& a) {
+    if (!a.xflag) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        atomicAdd_system(a.xflag, 1ull);
+    }
+}
+
 __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs a, int kind, int flag,
                                               int clear) {
     __shared__ double sh[16];
@@ -1181,11 +1196,13 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_ARN) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // = launcher's size
         post_arn(d, a, rec, d.RED1, d.RED2, Hs, h2s, sh);
+        post_signal(a);
         return;
     }
     if (kind == POST_ARN_D) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;
         post_arn_d(d, a, rec, Hs, h2s, qs, h1s, sh);
+        post_signal(a);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -1208,6 +1225,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         }
         if (flag) put_gram(rec, kmax, j, d.RED1 + 2, ld(d.RED1, 1), d.track_gram);
         else if (t == 0) st(rec, rec_col(kmax), -1.0);
+        post_signal(a);
         return;
     }
     if (kind == POST_LAN_FIN) {

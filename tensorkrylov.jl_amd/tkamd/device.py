@@ -131,6 +131,11 @@ class DeviceDecomposition:
         A_s, 2: CGS2), 0 for the Lanczos methods (tk_decomp_arnoldi_sweeps)."""
         return int(self.ctx._lib.tk_decomp_arnoldi_sweeps(self.h))
 
+    @property
+    def exchange_signalled(self):
+        """Records exchange triggered by a signal word, not an event (tk_decomp_exchange_signalled)."""
+        return bool(self.ctx._lib.tk_decomp_exchange_signalled(self.h))
+
     def _rec(self):
         return np.zeros((self.d_total, self.m))
 

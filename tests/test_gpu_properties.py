@@ -245,7 +245,7 @@ def test_tensorkrylov_nonsym_distinct_rhs_vs_oracle(ctx):
 
 
 # ------------------------------------------------------------------ exchange path (N > 1 code)
-@pytest.mark.parametrize("method", [0, 2])
+@pytest.mark.parametrize("method", [0, 1, 2])
 def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
     """The multi-rank path -- records summed by ncclAllReduce on the exchange stream, slot
     events, the receive buffer -- forced on a 1-rank communicator, gives bitwise the same
@@ -256,9 +256,11 @@ def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
     rng = np.random.default_rng(5)
     bs = [_unit(rng.random(n)) for _ in range(d)]
 
-    def run(c):
+    def run(c, sig=None):
         A = tk.DeviceMatrix(c, csc)
         dev = tk.DeviceDecomposition(c, method, d, 0, [A] * d, bs, K, track_all_gram=True)
+        if sig is not None:
+            assert dev.exchange_signalled == sig
         recs = [dev.init()] + [dev.step(j) for j in range(K)] + [dev.flush()]
         dev.init(False)                       # asynchronous sweep through the same path
         dev.sweep(0, K)
@@ -273,7 +275,9 @@ def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
     c2 = tk.Context(0)
     c2.init_comm(tk.unique_id(), 1, 0)
     monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
-    xch = run(c2)
+    # Arnoldi / Lanczos steps trigger the exchange through the signal word (the
+    # hipStreamWaitValue64 path), LanczosReorth through events
+    xch = run(c2, sig=method != 2)
     c2.close()
     for a, b in zip(local[0], xch[0]):
         assert np.array_equal(a, b)
