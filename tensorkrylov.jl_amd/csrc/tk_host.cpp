@@ -142,10 +142,29 @@ static bool tql(int n, Vec& d, Vec& e, Vec& Z) {
 
 static bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q) {
     Q.assign((size_t)n * n, 0.0);
-    for (int j = 0; j < n; ++j)
-        for (int i = j; i < n; ++i) Q[(size_t)j * n + i] = Q[(size_t)i * n + j] = A[(size_t)j * lda + i];   // lower
+    // Symmetric(H, :L) of an upper-Hessenberg H (Arnoldi) or of a Lanczos T is already
+    // tridiagonal: QL directly on (diag, subdiag), Q starting from the identity
+    bool tri = true;
+    for (int j = 0; j < n && tri; ++j)
+        for (int i = j + 2; i < n; ++i)
+            if (A[(size_t)j * lda + i] != 0.0) {
+                tri = false;
+                break;
+            }
     Vec e;
-    tridiagonalize(n, Q, w, e);
+    if (tri) {
+        w.assign(n, 0.0);
+        e.assign(n, 0.0);
+        for (int i = 0; i < n; ++i) {
+            w[i] = A[(size_t)i * lda + i];
+            if (i > 0) e[i] = A[(size_t)(i - 1) * lda + i];
+            Q[(size_t)i * n + i] = 1.0;
+        }
+    } else {
+        for (int j = 0; j < n; ++j)
+            for (int i = j; i < n; ++i) Q[(size_t)j * n + i] = Q[(size_t)i * n + j] = A[(size_t)j * lda + i];   // lower
+        tridiagonalize(n, Q, w, e);
+    }
     if (!tql(n, w, e, Q)) return false;
     // ascending order
     std::vector<int> idx(n);
@@ -358,6 +377,15 @@ tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* la
     auto y = [&](int s, int i, int j) { return Y[(size_t)s * kt + (size_t)j * k + i]; };
     // Ly_s = lower(Y_s' Y_s), Z_s = H_s Y_s, Lz_s = lower(Z_s' Z_s), X_s = Y_s' Z_s (t x t, [i*t+j])
     Vec Ly(d * tt, 0.0), Lz(d * tt, 0.0), X(d * tt, 0.0), Z((size_t)d * kt, 0.0);
+    // rows of H below the first subdiagonal are zero for the Hessenberg / tridiagonal minors
+    // the driver passes (checked: a general H is handled too)
+    int band = 1;
+    for (int s = 0; s < d && band < k; ++s) {
+        const double* Hs = H + (size_t)s * k * k;
+        for (int b = 0; b < k; ++b)
+            for (int a = b + band + 1; a < k; ++a)
+                if (Hs[(size_t)b * k + a] != 0.0) band = a - b;
+    }
     for (int s = 0; s < d; ++s) {
         const double* Hs = H + (size_t)s * k * k;
         double* Zs = &Z[(size_t)s * kt];
@@ -365,7 +393,8 @@ tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* la
             for (int b = 0; b < k; ++b) {
                 const double yb = y(s, b, j);
                 const double* hc = Hs + (size_t)b * k;
-                for (int a = 0; a < k; ++a) Zs[(size_t)j * k + a] += hc[a] * yb;
+                const int amax = std::min(k, b + band + 1);
+                for (int a = 0; a < amax; ++a) Zs[(size_t)j * k + a] += hc[a] * yb;
             }
         for (int i = 0; i < t; ++i)
             for (int j = 0; j < t; ++j) {
