@@ -535,6 +535,13 @@ struct tk_decomp {
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
     unsigned long long xcount = 0;
+    // single rank: records also land in host-mapped memory with a per-factor sequence word,
+    // so tk_decomp_records waits for exactly its steps (not for the whole queue)
+    double* hrec = nullptr;                 // [(kmax+2) slots][d_total][m]
+    unsigned long long* hdone = nullptr;    // [(kmax+2) slots][nf]
+    unsigned long long seq = 0;
+    std::vector<unsigned long long> slot_seq;   // per slot: seq of the signalled step that wrote it, 0 = none
+    hipStream_t cstream = nullptr;          // record copies (multi-rank): no wait on the compute queue
     int last_j = -1;
     std::vector<tk_mat*> mats;
     std::vector<DFac> hf;   // host copy of descriptors
@@ -569,6 +576,9 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
     if (dc->xflag) hipFree(dc->xflag);
+    if (dc->hrec) hipHostFree(dc->hrec);
+    if (dc->hdone) hipHostFree(dc->hdone);
+    if (dc->cstream) hipStreamDestroy(dc->cstream);
     delete dc;
 }
 
@@ -689,11 +699,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->ev_c.assign(kmax + 2, nullptr);
         dc->ev_x.assign(kmax + 2, nullptr);
         for (int i = 0; i < kmax + 2; ++i) {
-            // stream-order events between the compute and exchange streams of this device:
-            // kernel completion already releases at device scope; no system-scope fence
-            const unsigned fl = hipEventDisableTiming | hipEventDisableSystemFence;
-            hipError_t e = hipEventCreateWithFlags(&dc->ev_c[i], fl);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&dc->ev_x[i], fl);
+            // ev_c (compute -> exchange, only when the signal word is unavailable) needs no
+            // system-scope fence: kernel completion releases at device scope.  ev_x (exchange
+            // done) keeps it: the host waits on it and then copies the received records.
+            hipError_t e = hipEventCreateWithFlags(&dc->ev_c[i], hipEventDisableTiming | hipEventDisableSystemFence);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&dc->ev_x[i], hipEventDisableTiming);
             if (e != hipSuccess) {
                 free_decomp(dc);
                 return fail(TK_ERR_HIP, "hipEventCreate: %s", hipGetErrorString(e));
@@ -718,6 +728,28 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
         (void)hipGetLastError();   // an unsupported signal path must not leave a sticky error
+    }
+    dc->slot_seq.assign(kmax + 2, 0);
+    if (method != TK_LANCZOS_REORTH) {
+        if (dc->recv == dc->rec) {
+            void* hr = nullptr;
+            void* hd = nullptr;
+            const size_t nrec = (size_t)(kmax + 2) * d_total * dc->m;
+            if (hipHostMalloc(&hr, nrec * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+                hipHostMalloc(&hd, (size_t)(kmax + 2) * nf * sizeof(unsigned long long),
+                              hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+                memset(hr, 0, nrec * sizeof(double));
+                memset(hd, 0, (size_t)(kmax + 2) * nf * sizeof(unsigned long long));
+                dc->hrec = (double*)hr;
+                dc->hdone = (unsigned long long*)hd;
+            } else {
+                if (hr) hipHostFree(hr);
+                if (hd) hipHostFree(hd);
+            }
+        } else if (hipStreamCreateWithFlags(&dc->cstream, hipStreamNonBlocking) != hipSuccess) {
+            dc->cstream = nullptr;
+        }
+        (void)hipGetLastError();
     }
     c->refs++;
     for (tk_mat* A : dc->mats) A->refs++;
@@ -768,6 +800,9 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.gate = 0;
     a.ubuf = 0;
     a.xflag = nullptr;
+    a.hrec = nullptr;
+    a.hdone = nullptr;
+    a.seq = 0;
     return a;
 }
 
@@ -875,8 +910,15 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     tk_status st = slot_guard(dc, slot);
     if (st) return st;
     KArgs a = base_args(dc, j, slot);
-    KArgs ax = a;          // the step's last k_post signals the exchange stream
+    KArgs ax = a;          // the step's last k_post signals the exchange stream / the host
     ax.xflag = dc->xflag;
+    const bool hsig = dc->hdone && (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS);
+    dc->slot_seq[slot] = 0;
+    if (hsig) {
+        ax.hrec = dc->hrec + (size_t)slot * dc->d_total * dc->m;
+        ax.hdone = dc->hdone + (size_t)slot * nf;
+        ax.seq = ++dc->seq;
+    }
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
     if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
@@ -959,6 +1001,7 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
     if (sig) dc->xcount += (unsigned long long)dc->nf;   // the step's k_post adds one per factor
     tk_status st = step_impl(dc, j, rec_out);
     if (st) return st;
+    if (dc->hdone && (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS)) dc->slot_seq[j + 1] = dc->seq;
     return exchange_and_copy(dc, j + 1, rec_out, sig);
 }
 
@@ -1000,6 +1043,41 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
     CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
     HIPCHK(hipSetDevice(dc->ctx->device));
     const size_t per = (size_t)dc->d_total * dc->m;
+    if (s1 == s0) return TK_OK;
+    bool hosted = dc->hdone != nullptr;
+    for (int sl = s0; sl < s1 && hosted; ++sl) hosted = dc->slot_seq[sl] != 0;
+    if (hosted) {
+        // wait for the steps that wrote these slots only (later steps may be queued or
+        // running), then read their records from host-mapped memory
+        for (int sl = s0; sl < s1; ++sl) {
+            const unsigned long long want = dc->slot_seq[sl];
+            const unsigned long long* w = dc->hdone + (size_t)sl * dc->nf;
+            for (int f = 0; f < dc->nf; ++f) {
+                long spins = 0;
+                while (__atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want) {
+                    if (++spins % 4096 == 0) {
+                        // the device may have failed: surface its error instead of spinning
+                        hipError_t e = hipStreamQuery(dc->ctx->stream);
+                        if (e != hipSuccess && e != hipErrorNotReady)
+                            return fail(TK_ERR_HIP, "waiting for step records: %s", hipGetErrorString(e));
+                        if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)
+                            return fail(TK_ERR_STATE, "step records of slot %d never arrived", sl);
+                    }
+                }
+            }
+        }
+        memcpy(out, dc->hrec + (size_t)s0 * per, (s1 - s0) * per * sizeof(double));
+        return TK_OK;
+    }
+    if (dc->cstream && dc->recv != dc->rec) {
+        // multi-rank: the slots are final once the exchange of the last one has run
+        // (exchanges run in slot order on the exchange stream); copy on a stream of its own
+        HIPCHK(hipEventSynchronize(dc->ev_x[s1 - 1]));
+        HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
+                              dc->cstream));
+        HIPCHK(hipStreamSynchronize(dc->cstream));
+        return TK_OK;
+    }
     HIPCHK(hipStreamSynchronize(dc->ctx->xstream));
     HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                           dc->ctx->stream));

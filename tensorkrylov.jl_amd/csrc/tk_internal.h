@@ -80,6 +80,10 @@ struct KArgs {
     int ubuf;         // one-sweep Arnoldi: 0 = the pending raw vector u is in U, 1 = in W
     unsigned long long* xflag;   // non-null: each k_post block adds 1 once its record is
                                  // written (signal memory the exchange stream waits on)
+    double* hrec;                // non-null: the step's record slot in host-mapped memory
+                                 // ([d_total][m]); k_post copies its row there ...
+    unsigned long long* hdone;   // ... then stores `seq` to hdone[local factor] (host-mapped)
+    unsigned long long seq;
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register

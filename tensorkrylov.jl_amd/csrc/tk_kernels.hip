@@ -1142,12 +1142,23 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
 // are ordered before thread 0's device-scope release, then one system-scope add to the
 // signal word (the stream waits for the count of all of the step's blocks; no event marker
 // in the compute queue).
-__device__ __forceinline__ void post_signal(const KArgs& a) {
-    if (!a.xflag) return;
+__device__ __forceinline__ void post_signal(const KArgs& a, const DFac& d) {
+    if (!a.xflag && !a.hdone) return;
     __syncthreads();
+    if (a.hdone) {
+        // host mirror of the record row (host-mapped, coherent), then its sequence number:
+        // the host reads the record as soon as the word shows this step, without touching
+        // the queues (later steps may already be running)
+        const double* src = a.rec + (int64_t)d.gidx * a.m;
+        double* dst = a.hrec + (int64_t)d.gidx * a.m;
+        for (int i = threadIdx.x; i < a.m; i += TPB) dst[i] = ld(src, i);
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
         __threadfence_system();
-        atomicAdd_system(a.xflag, 1ull);
+        if (a.xflag) atomicAdd_system(a.xflag, 1ull);
+        if (a.hdone)
+            __hip_atomic_store(a.hdone + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1196,13 +1207,13 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_ARN) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // = launcher's size
         post_arn(d, a, rec, d.RED1, d.RED2, Hs, h2s, sh);
-        post_signal(a);
+        post_signal(a, d);
         return;
     }
     if (kind == POST_ARN_D) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;
         post_arn_d(d, a, rec, Hs, h2s, qs, h1s, sh);
-        post_signal(a);
+        post_signal(a, d);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -1225,7 +1236,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         }
         if (flag) put_gram(rec, kmax, j, d.RED1 + 2, ld(d.RED1, 1), d.track_gram);
         else if (t == 0) st(rec, rec_col(kmax), -1.0);
-        post_signal(a);
+        post_signal(a, d);
         return;
     }
     if (kind == POST_LAN_FIN) {

@@ -18,16 +18,17 @@ from .structures import ConvergenceData, KruskalTensor, kronprodnorm
 
 
 def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbose=False,
-                 backend=None, keep_decomposition=False, pipelined=True):
+                 backend=None, keep_decomposition=False, pipelined=True, depth=2):
     """tensorkrylov!(convergence_data, A, b, tol, nmax, orthonormalization_type).
     Returns the approximate solution as a KruskalTensor of the LOCAL factors
     (x_s = V_s y_s) on convergence, else None.
 
-    pipelined: step k+1 is enqueued on the device before the host evaluates iteration k
-    (compressed solve, residual), so device and host work overlap.  Step k+1 leaves
-    V[:, 1:k], H[1:k, 1:k] and b~[1:k] untouched, so every iterate, residual and the
-    returned solution are those of the sequential loop; on convergence at k the extra
-    step's result is simply never read."""
+    pipelined: steps k+1 .. k+depth are enqueued on the device before the host evaluates
+    iteration k (compressed solve, residual), so device and host work overlap and the
+    device never waits for the host's read of a record.  Steps after k leave V[:, 1:k],
+    H[1:k, 1:k] and b~[1:k] untouched, so every iterate, residual and the returned solution
+    are those of the sequential loop; on convergence at k the extra steps' results are
+    simply never read."""
     if isinstance(method, str):
         method = METHODS[method]
     d = len(A)
@@ -43,13 +44,15 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
         conv.timing["setup_s"] = t_loop - t_start                   # upload A_s, b_s; step 1
         spectral = SpectralData(A, nmax)                            # :57
         approx = ApproximationData(tol, symmetric)                  # :58
-        if pipelined and nmax >= 2:
-            td.issue(2)
+        depth = max(1, int(depth))
+        if pipelined:
+            for kk in range(2, min(nmax, 1 + depth) + 1):
+                td.issue(kk)
         for k in range(2, nmax + 1):                                # :63
             if pipelined:
                 td.collect(k)                                       # :66
-                if k + 1 <= nmax:
-                    td.issue(k + 1)                                 # overlaps the host work below
+                if k + depth <= nmax:
+                    td.issue(k + depth)                             # overlaps the host work below
             else:
                 td.orthonormalize(k)                                # :66
             Hm = td.minors(k)                                       # :68
