@@ -52,14 +52,15 @@ def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None):
     """algorithmic bytes of one factor-step with k basis columns (int32 CSR).
     Arnoldi as two-sweep CGS2 (sweeps=2): B_spmv + 2 MGS passes + write V_{k+1} + the RHS
     dot.  One-sweep Arnoldi (sweeps=1, delayed reorthogonalization):
-    V_1..V_{k-1} read once + the raw vector u read and written + V_k written + b read
-    (both SpMVs take their vector from LDS) + the matrix bytes its storage must read
+    V_1..V_{k-1} read once + the raw vector u read and written + V_k written (both SpMVs
+    take their vector from LDS; <V_k, b> = norm(b) <V_k, V_1> needs no read of b) + the
+    matrix bytes its storage must read
     (`mat_bytes`: 0 for a Toeplitz band, whose diagonals are 4 scalars).  Lanczos: B_spmv +
     read V_{k-1} + write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new
     column, 8n(k+1) (its redo steps are extra work, not counted)."""
     b_spmv = 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n
     if method == "TensorArnoldi" and sweeps == 1:
-        return 8 * n * (k - 1) + 4 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
+        return 8 * n * (k - 1) + 3 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
     if method == "TensorArnoldi":
         return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
     b = b_spmv + 8 * n + 8 * n + 8 * n

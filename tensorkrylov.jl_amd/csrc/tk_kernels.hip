@@ -584,8 +584,8 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
 //   v_j     = (u_j - V[:,0..j) c) * inv_beta                      -> V[:, j]
 //   u_{j+1} = A v_j - V[:,0..j) h1[0..j) - h1[j] v_j               -> the other buffer
 //   z       = A u_{j+1}
-//   P1 = [ <V[:,c],u> (c<j) | <V[:,c],z> (c<j) | <v_j,u>, <v_j,z>, <u,u>, <u,z>, <v_j,b>,
-//          <v_j,v_j> | gram <V[:,c],v_j> (c<j) ]
+//   P1 = [ <V[:,c],u> (c<j) | <V[:,c],z> (c<j) | <v_j,u>, <v_j,z>, <u,u>, <u,z>, <v_j,v_0>,
+//          <v_j,v_j> | gram <V[:,c],v_j> (c<j) ]       (<v_j,b> = norm(b) <v_j,v_0> in the post)
 // Both SpMVs read their vector from LDS, so each block works on an overlapping window of
 // 256 rows and owns the middle 256 - 2(hl+hu) of them: v_j is valid on the whole window,
 // u on all but hl/hu rows at its edges, z on all but 2hl/2hu -- the owned rows.  Halo rows
@@ -702,7 +702,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             st(Uout, r, u);
         }
         const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
-        const double bv = own ? ld(d.b, r) : 0.0;
+        // update_rhs!'s <v_j, b> as norm(b) * <v_j, v_0> (b = norm(b) v_0, src/decompositions.jl:
+        // 112-118): v_0 is column 0 of the register row, so b is not read (-8 B per row)
+        const double v0r = j > 0 ? R.v[0] : vj;
 #ifndef TK_D1_NORED   // (timing experiment: column dots skipped)
 #pragma unroll
         for (int k = 0; k < NUZ; ++k) {
@@ -729,12 +731,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         }
 #endif
         {
-            double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * bv, vo * vj};
+            double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
             acc[NUZ * TPB + t] += rs16(x);
         }
     }
     // combine the 16 row-group partials of every value (fixed order) -> P1
-    //   [ p (c<j) | q (c<j) | p_j, q_j, |u|^2, <u,z>, bt_j, gram_jj | gram (c<j) ]
+    //   [ p (c<j) | q (c<j) | p_j, q_j, |u|^2, <u,z>, <v_j,v_0>, gram_jj | gram (c<j) ]
     __syncthreads();
     for (int e = t; e < nch * 16; e += TPB) {
         const int k = e >> 4, sl = e & 15;
@@ -1042,8 +1044,9 @@ __device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const doubl
 }
 
 // One-sweep Arnoldi post-processing of step j.  RED1 holds (k_arn_d1)
-//   p = <V[:,c],u> (c<j) | q = <V[:,c],z> (c<j) | p_j, q_j, |u|^2, <u,z>, bt_j, gram_jj | gram (c<j)
-// with u = u_{j+1}, z = A u.  The reorthogonalization coefficients of u are c = p; then
+//   p = <V[:,c],u> (c<j) | q = <V[:,c],z> (c<j) | p_j, q_j, |u|^2, <u,z>, <v_j,v_0>, gram_jj |
+//   gram (c<j)
+// with u = u_{j+1}, z = A u; bt_j = norm(b) <v_j,v_0>.  The reorthogonalization coefficients of u are c = p; then
 //   H[0..j, j] = h1 + c,  beta = H[j+1, j] = sqrt(|u|^2 - |c|^2)        (CGS2 of
 //   src/orthogonal_bases.jl:22-36 in exact arithmetic),  v_{j+1} = (u - V c) * inv(beta),
 // and the first projection of A v_{j+1} = (z - V Hbar c) * inv(beta) (Arnoldi relation for
@@ -1132,7 +1135,7 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
         for (int i = t; i <= j; i += TPB) st(rec, rec_gram(kmax) + i, i < j ? ld(R, 2 * j + 6 + i) : ld(R, 2 * j + 5));
     }
     if (t == 0) {
-        st(rec, rec_bt(kmax), ld(R, 2 * j + 4));
+        st(rec, rec_bt(kmax), ld(d.sc, SC_BNORM) * ld(R, 2 * j + 4));   // norm(b) <v_j, v_0>
         st(rec, rec_col(kmax), (double)j);
         st(rec, rec_tracked(kmax), d.track_gram ? 1.0 : 0.0);
     }
