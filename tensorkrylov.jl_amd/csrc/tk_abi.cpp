@@ -730,7 +730,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         (void)hipGetLastError();   // an unsupported signal path must not leave a sticky error
     }
     dc->slot_seq.assign(kmax + 2, 0);
-    if (method != TK_LANCZOS_REORTH) {
+    {
         if (dc->recv == dc->rec) {
             void* hr = nullptr;
             void* hd = nullptr;
@@ -912,7 +912,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     KArgs a = base_args(dc, j, slot);
     KArgs ax = a;          // the step's last k_post signals the exchange stream / the host
     ax.xflag = dc->xflag;
-    const bool hsig = dc->hdone && (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS);
+    const bool hsig = dc->hdone != nullptr;
     dc->slot_seq[slot] = 0;
     if (hsig) {
         ax.hrec = dc->hrec + (size_t)slot * dc->d_total * dc->m;
@@ -984,6 +984,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, g, s), "arn_finalize");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s, 1), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, g, POST_ARN_FIN, 0, 0, s), "post");
+        // the record is final only after the gated redo: one ungated launch mirrors it to
+        // the host (the exchange of a LanczosReorth handle waits on an event instead)
+        if (hsig) RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_SIGNAL, 0, 0, s), "post_signal");
         dc->pending = false;
     }
     dc->last_j = j;
@@ -1001,7 +1004,7 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
     if (sig) dc->xcount += (unsigned long long)dc->nf;   // the step's k_post adds one per factor
     tk_status st = step_impl(dc, j, rec_out);
     if (st) return st;
-    if (dc->hdone && (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS)) dc->slot_seq[j + 1] = dc->seq;
+    if (dc->hdone) dc->slot_seq[j + 1] = dc->seq;
     return exchange_and_copy(dc, j + 1, rec_out, sig);
 }
 

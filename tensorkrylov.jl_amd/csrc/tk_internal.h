@@ -118,7 +118,8 @@ enum PostKind {
     POST_ARN_FIN = 3,    // after arn_finalize (column j+1)
     POST_LAN = 4,        // after l2; fused flag in `flag`
     POST_LAN_FIN = 5,    // after lan_finalize (column j+1)
-    POST_ARN_D = 6       // after k_arn_d1 (one-sweep Arnoldi): H column j, c, beta, next h1
+    POST_ARN_D = 6,      // after k_arn_d1 (one-sweep Arnoldi): H column j, c, beta, next h1
+    POST_SIGNAL = 7      // only mirror the finished record to the host (LanczosReorth)
 };
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s);
 void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s);

@@ -1174,6 +1174,10 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
     if (a.gate && ld(d.sc, SC_REDO) == 0.0) return;
+    if (kind == POST_SIGNAL) {
+        post_signal(a, d);
+        return;
+    }
     const int j = a.j, kmax = a.kmax;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
     const int t = threadIdx.x;
