@@ -527,6 +527,7 @@ struct tk_decomp {
     int jnext = 0;          // next step index
     int fmt = 0;            // SpMV storage shared by all local factors (KArgs::fmt)
     bool onesweep = false;  // Arnoldi as one sweep per step (k_arn_d1): banded A_s only
+    bool fin_d = true;      // ungated column writes through k_fin_d (TKHIP_FIN_D=0: tile-loop kernels)
     int npd = 0;            // max DFac::npd over the local factors (grid width of k_arn_d1)
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
@@ -633,6 +634,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->onesweep = ok;
     }
     dc->nvmax = dc->onesweep ? 3 * kmax + 8 : 2 * kmax + 8;
+    {
+        const char* e = getenv("TKHIP_FIN_D");
+        dc->fin_d = !(e && e[0] == '0');
+    }
     dc->mats.assign(mats, mats + nf);
     dc->hf.resize(nf);
     const int KP = kmax + 2, KC = kmax + 1;
@@ -659,7 +664,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             d.npd = wpb >= 1 ? (d.nwin + wpb - 1) / wpb : (d.nwin + std::max(1, d.nwin / npcap) - 1) / std::max(1, d.nwin / npcap);
         }
         dc->npd = std::max(dc->npd, d.npd);
-        const int npp = std::max(dc->npart, dc->onesweep ? d.npd : 0);
+        const int npp = std::max(std::max(dc->npart, dc->onesweep ? d.npd : 0), dc->ntiles);
         DA(d.V, (size_t)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double));   // tile-major, paired columns
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
@@ -888,15 +893,25 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
     tk_ctx* c = dc->ctx;
     hipStream_t s = c->stream;
     const int nf = dc->nf, j = a.j;
+    const bool fd = dc->fin_d && j + 1 <= D1_JMAX;
+    const int np = fd ? dc->ntiles : dc->npart;
     if (dc->method == TK_ARNOLDI) {
         KArgs f = a;
         if (dc->onesweep && j <= D1_JMAX) f.ubuf = (j & 1) ? 0 : 1;   // one-sweep step j wrote u_{j+1} to U (j odd) or W
-        RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, f, s), "arn_finalize");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        if (fd) {
+            RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, f, 0, s), "fin_d");
+        } else {
+            RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, f, s), "arn_finalize");
+        }
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, np, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, 1, s), "post");
     } else {
-        RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        if (fd) {
+            RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, a, 1, s), "fin_d");
+        } else {
+            RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
+        }
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, np, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 0, 1, s), "post");
     }
     return TK_OK;
@@ -971,8 +986,13 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_PASS2, 2, launch_lan_l2(dc->df, nf, a, s), "lan_l2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 1, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN, 0, 1, s), "post");
-        RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        if (dc->fin_d && j + 1 <= D1_JMAX) {
+            RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, a, 1, s), "fin_d");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->ntiles, s), "reduce");
+        } else {
+            RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
+        }
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_LAN_FIN, 1, 0, s), "post");
         KArgs g = a;
         g.gate = 1;

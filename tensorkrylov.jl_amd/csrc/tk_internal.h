@@ -108,6 +108,9 @@ void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+// ungated write of the pending column j+1 for j + 1 <= 64 columns (mode 0 Arnoldi, 1 Lanczos):
+// one partial per tile (reduce with npart = ntiles)
+void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s);
 // npart <= 0: each factor's own DFac::npd partials (one-sweep Arnoldi)
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0);
 // post-processing (one 64-thread block per factor)

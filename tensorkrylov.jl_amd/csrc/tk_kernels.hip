@@ -787,6 +787,96 @@ __global__ __launch_bounds__(TPB) void k_init_bd(const DFac* __restrict__ F, KAr
     store_partials(acc, d.P1, d.npd, 3);
 }
 
+// Write the pending column j+1 (the flush of every method, and LanczosReorth's per-step
+// write of v_{j+1}) with the one-sweep kernel's reductions: one 256-row tile per block,
+// XCD-aware tile slots, column dots reduce-scattered by DPP into private LDS slots, one
+// partial per tile.  MODE 0 (Arnoldi): v = (u - V[:,0..j] h2) * inv(beta) from U or W;
+//   P1 = [ gram <V[:,c],v> (c<=j, tracked factors) | <v,v> | <v,b> ]      (POST_ARN_FIN)
+// MODE 1 (Lanczos TTR): v = (beta == 0 ? 0 : inv(beta) .* W) (src/orthogonal_bases.jl:59);
+//   P1 = [ <v,b> | gram <V[:,c],v> (c<=j) | <v,v> ]  (gram and <v,v>: tracked)  (POST_LAN_FIN)
+// For j + 1 <= 64 columns (the register row); beyond, and for gated launches, the
+// tile-loop kernels above.
+template <int MAXC, int MODE>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
+void k_fin_d(const DFac* __restrict__ F, KArgs a) {
+    constexpr int NG = (MAXC + 15) / 16;
+    extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
+    const DFac& d = F[blockIdx.y];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= a.ntiles) return;
+    const int j = a.j, nc = j + 1, t = threadIdx.x;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    const int64_t r = (int64_t)slot * TPB + t;
+    const bool ok = r < a.n;
+    const double* Vt = d.V + (int64_t)slot * TS;
+    const uint32_t toff = t * 16u;
+    const rsrc_t tv = mkrsrc(Vt, vrange(nc));
+    const bool gram = d.track_gram != 0;
+    double* acc = lds;
+    const double inv_beta = ld(d.sc, SC_INVBETA);
+    if (MODE == 1 && !gram) {
+        // Lanczos without a Gram row: v, the pair store (other half = column j), <v,b>
+        const bool zero = ld(d.sc, SC_BETA) == 0.0;
+        const double v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+        const double other = ((j + 1) & 1) ? bld(tv, toff + cofs(j)) : 0.0;
+        st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, other);
+        double x[16] = {v * ld(d.b, r)};
+        acc[t] = rs16(x);
+        __syncthreads();
+        if (t == 0) {
+            double sum = 0.0;
+#pragma unroll
+            for (int p = 0; p < 16; ++p) sum += acc[p * 16];
+            st(d.P1, slot, sum);   // vi = 0
+        }
+        return;
+    }
+    Row<MAXC> R;
+    R.load(tv, toff, nc);
+    double v;
+    if (MODE == 0) {
+        const double up = ld(a.ubuf ? d.W : d.U, r);
+        v = ok ? (up - row_dot<MAXC, true>(R, tv, toff, nc, d.h2)) * inv_beta : 0.0;
+    } else {
+        const bool zero = ld(d.sc, SC_BETA) == 0.0;
+        v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+    }
+    st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, ((j + 1) & 1) ? R.last : 0.0);
+    if (gram) {
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            double x[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = 16 * k + i < MAXC ? R.v[16 * k + i < MAXC ? 16 * k + i : 0] * v : 0.0;
+            acc[k * TPB + t] = rs16(x);
+        }
+    }
+    {
+        double x[16] = {v * v, v * ld(d.b, r)};
+        acc[NG * TPB + t] = rs16(x);
+    }
+    __syncthreads();
+    // combine the 16 row-group partials of every value in fixed order
+    for (int e = t; e < (NG + 1) * 16; e += TPB) {
+        const int k = e >> 4, sl = e & 15;
+        if (k < NG && !gram) continue;
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) sum += acc[k * TPB + p * 16 + sl];
+        int vi = -1;
+        if (k < NG) {
+            const int c = 16 * k + sl;
+            if (c < nc) vi = MODE == 0 ? c : 1 + c;
+        } else if (sl == 0) {            // <v,v>
+            if (MODE == 0) vi = nc;
+            else if (gram) vi = 1 + nc;
+        } else if (sl == 1) {            // <v,b>
+            vi = MODE == 0 ? nc + 1 : 0;
+        }
+        if (vi >= 0) st(d.P1, (int64_t)vi * a.ntiles + slot, sum);
+    }
+}
+
 // ------------------------------------------------------------------ Lanczos (TTR)
 
 // Plain, v_j stored (src/orthogonal_bases.jl:45-50):
@@ -918,12 +1008,12 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 // Same for the one-sweep kernel's per-window partials (npart = DFac::npd, ~4k at n = 2^20):
 // four waves per value, each lane a strided subset in rounds of 16 independent loads, DPP
 // row sums, the 16 row totals summed in fixed order.
-__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv) {
+__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np) {
     __shared__ double rs[16];
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
     if (c >= nv) return;
-    const int npart = d.npd;
+    const int npart = np > 0 ? np : d.npd;
     const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
     const int t = threadIdx.x;
     double s = 0.0;
@@ -1479,12 +1569,24 @@ void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
+void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s) {
+    const int nc = a.j + 1;
+    const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
+    const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
+    const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
+    with_maxc(nc, [&](auto Mc) {
+        if (mode == 0) hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 0>), grid, dim3(TPB), lds, s, F, a);
+        else hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 1>), grid, dim3(TPB), lds, s, F, a);
+    });
+}
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate) {
     if (npart <= 0 && !gate)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv);
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0);
+    else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart);
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
