@@ -610,6 +610,14 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 // combined once, after the last window.  Chunk k < NUZ holds columns 8k..8k+7 times
 // (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row (16 columns
 // each).  acc[chunk][256]: slot t = (16-row group p = t >> 4, value s = t & 15).
+#if TK_D1_TRACE
+// diagnostic builds only (tools/build_variant.sh NAME - -DTK_D1_TRACE=1, tools/d1_trace.py):
+// per-block start / end wall clock (100 MHz) and HW_ID / XCC_ID of one step's k_arn_d1
+// launch, factor 0
+#define TRACE_MAX 8192
+__device__ int g_trace_j = -1;
+__device__ uint64_t g_trace[3 * TRACE_MAX];
+#endif
 template <int MAXC, int FMT>
 #ifndef TK_D1_OCCT
 #define TK_D1_OCCT 1
@@ -638,6 +646,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #else
     if ((int)blockIdx.x >= d.npd) return;
     const int slot = blockIdx.x;
+#endif
+#if TK_D1_TRACE
+    const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     double* acc = lds;
@@ -755,6 +766,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         }
         if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
     }
+#if TK_D1_TRACE
+    __syncthreads();
+    if (t == 0 && blockIdx.y == 0 && j == g_trace_j && slot < TRACE_MAX) {
+        g_trace[3 * slot] = trace_t0;
+        g_trace[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+        g_trace[3 * slot + 2] = ((uint64_t)__builtin_amdgcn_s_getreg(63508) << 32) | __builtin_amdgcn_s_getreg(63492);
+    }
+#endif
 }
 
 // Initialization for the one-sweep Arnoldi: V[:,0] = U = inv(norm(b)) .* b
@@ -1145,43 +1164,47 @@ __device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const doubl
 //   h1'[j+1] = ((<u,z> - c.q) * inv(beta) - (Hbar c)_{j+1}) * inv(beta)
 // c -> h2, h1' -> g (the next sweep's coefficients), inv(beta) -> scalars, the step's
 // record (H column j, beta, bt_j and the Gram row of column j).
-__device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* Hs, double* cs, double* qs,
-                           double* h1s, double* sh) {
-    const int j = a.j, kmax = a.kmax, KP = kmax + 2;
+__device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* Hs, double* red, double* h1s,
+                           double* row, double* sh) {
+    const int j = a.j, kmax = a.kmax;
     const int t = threadIdx.x;
-    const double* R = d.RED1;
-    double* Hc = d.H + (int64_t)j * KP;
-    const int J2 = j + 2;
+    double* Hc = d.H + (int64_t)j * (kmax + 2);
+    const int J2 = j + 2, nv = 3 * j + 6;
     // every global load of the kernel in one round trip: Hbar[:, 0..j) (16 per thread in
-    // flight; a loop beyond j = 62), the reduced dots and the current h1
-    if (Hs)
-        for (int i0 = 0; i0 < j * J2; i0 += 16 * TPB) {
-            double hv[16];
+    // flight; j <= 64 fits), the reduced dots, the current h1 and norm(b).  The record row is
+    // assembled in LDS (row) and written out once.
+    for (int i0 = 0; i0 < j * J2; i0 += 16 * TPB) {
+        double hv[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int idx = i0 + q * TPB + t;
-                const int i = idx / J2, l = idx - i * J2;
-                hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * KP + l) : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < 16; ++q)
-                if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
+        for (int q = 0; q < 16; ++q) {
+            const int idx = i0 + q * TPB + t;
+            const int i = idx / J2, l = idx - i * J2;
+            hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * (kmax + 2) + l) : 0.0;
         }
-    for (int i = t; i <= j; i += TPB) {
-        cs[i] = i < j ? ld(R, i) : ld(R, 2 * j);
-        qs[i] = i < j ? ld(R, j + i) : ld(R, 2 * j + 1);
-        h1s[i] = ld(d.g, i);
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
     }
+    for (int i = t; i < nv; i += TPB) red[i] = ld(d.RED1, i);
+    for (int i = t; i <= j; i += TPB) h1s[i] = ld(d.g, i);
+    for (int i = t; i < a.m; i += TPB) row[i] = 0.0;
+    if (t == 0) sh[10] = ld(d.sc, SC_BNORM);
     __syncthreads();
+    // c (p_l, l < j, then p_j) and q likewise
+    const double* cp = red;
+    const double* qp = red + j;
     double cc = 0.0, cq = 0.0;
     for (int i = t; i <= j; i += TPB) {
-        const double hv = h1s[i] + cs[i];
+        const double ci = i < j ? cp[i] : red[2 * j];
+        const double qi = i < j ? qp[i] : red[2 * j + 1];
+        const double hv = h1s[i] + ci;
         st(Hc, i, hv);
-        st(d.h2, i, cs[i]);
-        st(rec, i, hv);
-        if (Hs) Hs[j * J2 + i] = hv;
-        cc += cs[i] * cs[i];
-        cq += cs[i] * qs[i];
+        st(d.h2, i, ci);
+        row[i] = hv;
+        Hs[j * J2 + i] = hv;
+        h1s[i] = ci;   // c, for the Hbar c products below
+        cc += ci * ci;
+        cq += ci * qi;
     }
     cc = row16_sum(cc);
     cc += __shfl_xor(cc, 16);
@@ -1196,38 +1219,46 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
     __syncthreads();
     if (t == 0) {
         const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-        const double bsq = ld(R, 2 * j + 2) - s2;
+        const double bsq = red[2 * j + 2] - s2;
         const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
         st(Hc, j + 1, beta);
-        if (Hs) Hs[j * J2 + j + 1] = beta;
-        st(rec, j + 1, beta);
-        st(rec, rec_beta(kmax), beta);
+        Hs[j * J2 + j + 1] = beta;
+        row[j + 1] = beta;
+        row[rec_beta(kmax)] = beta;
         st(d.sc, SC_BETA, beta);
         st(d.sc, SC_INVBETA, 1.0 / beta);
         st(d.sc, SC_BETAPREV, beta);
         sh[8] = beta;
         sh[9] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
-    }
-    __syncthreads();
-    const double beta = sh[8], ib = 1.0 / beta;
-    for (int l = t; l <= j + 1; l += TPB) {
-        double s = 0.0;
-        for (int i = (l > 0 ? l - 1 : 0); i <= j; ++i) {
-            const double hv = Hs ? Hs[i * J2 + l]
-                                 : (i == j ? (l == j + 1 ? beta : ld(Hc, l)) : ld(d.H, (int64_t)i * KP + l));
-            s += hv * cs[i];
-        }
-        const double h = l <= j ? (qs[l] - s) * ib : ((ld(R, 2 * j + 3) - sh[9]) * ib - s) * ib;
-        st(d.g, l, h);
+        row[rec_bt(kmax)] = sh[10] * red[2 * j + 4];   // norm(b) <v_j, v_0>
+        row[rec_col(kmax)] = (double)j;
+        row[rec_tracked(kmax)] = d.track_gram ? 1.0 : 0.0;
     }
     // Gram row of column j: [gram (c<j), gram_jj]
-    if (d.track_gram) {
-        for (int i = t; i <= j; i += TPB) st(rec, rec_gram(kmax) + i, i < j ? ld(R, 2 * j + 6 + i) : ld(R, 2 * j + 5));
+    if (d.track_gram)
+        for (int i = t; i <= j; i += TPB) row[rec_gram(kmax) + i] = i < j ? red[2 * j + 6 + i] : red[2 * j + 5];
+    __syncthreads();
+    // h1'[l] from (Hbar c)_l: four lanes per l over interleaved i, combined in fixed order
+    const double beta = sh[8], ib = 1.0 / beta;
+    for (int l0 = 0; l0 <= j + 1; l0 += TPB / 4) {
+        const int l = l0 + (t >> 2), r = t & 3;
+        double sum = 0.0;
+        if (l <= j + 1)
+            for (int i = (l > 0 ? l - 1 : 0) + r; i <= j; i += 4) sum += Hs[i * J2 + l] * h1s[i];
+        sum += __shfl_xor(sum, 1);
+        sum += __shfl_xor(sum, 2);
+        if (r == 0 && l <= j + 1) {
+            const double h = l <= j ? ((l < j ? qp[l] : red[2 * j + 1]) - sum) * ib
+                                    : ((red[2 * j + 3] - sh[9]) * ib - sum) * ib;
+            st(d.g, l, h);
+        }
     }
-    if (t == 0) {
-        st(rec, rec_bt(kmax), ld(d.sc, SC_BNORM) * ld(R, 2 * j + 4));   // norm(b) <v_j, v_0>
-        st(rec, rec_col(kmax), (double)j);
-        st(rec, rec_tracked(kmax), d.track_gram ? 1.0 : 0.0);
+    __syncthreads();
+    // the record row, and its host mirror
+    double* hr = a.hdone ? a.hrec + (int64_t)d.gidx * a.m : nullptr;
+    for (int i = t; i < a.m; i += TPB) {
+        st(rec, i, row[i]);
+        if (hr) hr[i] = row[i];
     }
 }
 
@@ -1235,10 +1266,10 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
 // are ordered before thread 0's device-scope release, then one system-scope add to the
 // signal word (the stream waits for the count of all of the step's blocks; no event marker
 // in the compute queue).
-__device__ __forceinline__ void post_signal(const KArgs& a, const DFac& d) {
+__device__ __forceinline__ void post_signal(const KArgs& a, const DFac& d, bool mirrored = false) {
     if (!a.xflag && !a.hdone) return;
     __syncthreads();
-    if (a.hdone) {
+    if (a.hdone && !mirrored) {
         // host mirror of the record row (host-mapped, coherent), then its sequence number:
         // the host reads the record as soon as the word shows this step, without touching
         // the queues (later steps may already be running)
@@ -1271,7 +1302,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     const int j = a.j, kmax = a.kmax;
     double* rec = a.rec + (int64_t)d.gidx * a.m;
     const int t = threadIdx.x;
-    if (clear) {
+    if (clear && kind != POST_ARN_D) {   // (POST_ARN_D writes the whole row)
         for (int i = t; i < a.m; i += TPB) st(rec, i, 0.0);
         __syncthreads();
     }
@@ -1308,9 +1339,9 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         return;
     }
     if (kind == POST_ARN_D) {
-        double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;
-        post_arn_d(d, a, rec, Hs, h2s, qs, h1s, sh);
-        post_signal(a, d);
+        // dynamic LDS: Hbar ((j+1)(j+2) doubles, j <= 64), then the record row (m)
+        post_arn_d(d, a, rec, post_lds, qs, h1s, post_lds + (((a.j + 1) * (a.j + 2) + 1) & ~1), sh);
+        post_signal(a, d, true);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -1592,7 +1623,8 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
 }
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
-    const size_t lds = ((kind == POST_ARN || kind == POST_ARN_D) && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
+    size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
+    if (kind == POST_ARN_D) lds = (size_t)((((a.j + 1) * (a.j + 2) + 1) & ~1) + a.m) * sizeof(double);
     hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), lds, s, F, a, kind, flag, clear);
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
@@ -1616,3 +1648,11 @@ void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, doubl
 }
 
 }  // namespace tk
+
+#if TK_D1_TRACE
+extern "C" int tk_debug_d1_trace(int j, uint64_t* out, int n) {
+    if (!out) return (int)hipMemcpyToSymbol(HIP_SYMBOL(tk::g_trace_j), &j, sizeof(int));
+    hipDeviceSynchronize();
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tk::g_trace), sizeof(uint64_t) * 3 * (n < TRACE_MAX ? n : TRACE_MAX));
+}
+#endif
