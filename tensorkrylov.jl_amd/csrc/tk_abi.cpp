@@ -965,7 +965,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;
-        if (fused) {
+        if (fused && dc->fin_d && j >= 1 && j <= D1_JMAX) {
+            RUN(TCLS_PASS1, 2, launch_lan_d1(dc->df, nf, a, s), "lan_d1");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->ntiles, s), "reduce");
+        } else if (fused) {
             RUN(TCLS_PASS1, 2, launch_lan_l1_fused(dc->df, nf, a, s), "lan_l1_fused");
             RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s), "reduce");
         } else {

@@ -106,6 +106,7 @@ void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t 
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
+void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s);   // j in 1..64
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 // ungated write of the pending column j+1 for j + 1 <= 64 columns (mode 0 Arnoldi, 1 Lanczos):

@@ -29,6 +29,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "tk_internal.h"
@@ -953,6 +954,88 @@ __global__ __launch_bounds__(TPB) void k_lan_l1_fused(const DFac* __restrict__ F
     store_partials(acc, d.P1, a.npart, gram ? j + 3 : 2);
 }
 
+// The same step as k_lan_l1_fused for j <= 64, laid out like k_fin_d: one tile per block
+// (XCD-aware slots), the tracked factor's Gram row from a register row of V[:, 0..j) with DPP
+// reduce-scatters, one partial per tile.  The Gram row was the long pole of the tile-loop
+// kernel: factor 1's 1024 blocks streamed it through LDS transposes while the other factors'
+// blocks had long finished.
+//   P1 = [ <U,v_j>, <v_j,b> | gram <V[:,c],v_j> (c<j), <v_j,v_j> ]   (as k_lan_l1_fused)
+template <int MAXC, int FMT>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
+void k_lan_d1(const DFac* __restrict__ F, KArgs a) {
+#pragma clang fp contract(off)
+    constexpr int NG = (MAXC + 15) / 16;
+    extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
+    const DFac& d = F[blockIdx.y];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= a.ntiles) return;
+    const int j = a.j, t = threadIdx.x;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    const int64_t r = (int64_t)slot * TPB + t;
+    const bool ok = r < a.n;
+    const double* Vt = d.V + (int64_t)slot * TS;
+    const uint32_t toff = t * 16u;
+    const rsrc_t tv = mkrsrc(Vt, vrange(j));
+    const bool gram = d.track_gram != 0;
+    double* acc = lds;
+    const double beta = ld(d.sc, SC_BETA);
+    const double inv_beta = ld(d.sc, SC_INVBETA);
+    const bool zero = (beta == 0.0);
+    const double vj = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+    const double* Wg = d.W;
+    const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return zero ? 0.0 : mul_rn(ld(Wg, c), inv_beta); }) : 0.0;
+    if (!gram) {
+        const double vprev = bld(tv, toff + cofs(j - 1));
+        const double u = av - beta * vprev;
+        st_pair(d.V, (int64_t)slot * TS, j, t, vj, (j & 1) ? vprev : 0.0);
+        st(d.U, r, u);
+        double x[16] = {u * vj, vj * ld(d.b, r)};
+        acc[t] = rs16(x);
+        __syncthreads();
+        if (t < 2) {
+            double sum = 0.0;
+#pragma unroll
+            for (int p = 0; p < 16; ++p) sum += acc[p * 16 + t];
+            st(d.P1, (int64_t)t * a.ntiles + slot, sum);
+        }
+        return;
+    }
+    Row<MAXC> R;
+    R.load(tv, toff, j);
+    const double vprev = R.last;   // column j - 1
+    const double u = av - beta * vprev;
+    st_pair(d.V, (int64_t)slot * TS, j, t, vj, (j & 1) ? vprev : 0.0);
+    st(d.U, r, u);
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+        double x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = 16 * k + i < MAXC ? R.v[16 * k + i < MAXC ? 16 * k + i : 0] * vj : 0.0;
+        acc[k * TPB + t] = rs16(x);
+    }
+    {
+        double x[16] = {u * vj, vj * ld(d.b, r), vj * vj};
+        acc[NG * TPB + t] = rs16(x);
+    }
+    __syncthreads();
+    for (int e = t; e < (NG + 1) * 16; e += TPB) {
+        const int k = e >> 4, sl = e & 15;
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < 16; ++p) sum += acc[k * TPB + p * 16 + sl];
+        int vi = -1;
+        if (k < NG) {
+            const int c = 16 * k + sl;
+            if (c < j) vi = 2 + c;
+        } else if (sl < 2) {
+            vi = sl;             // <U,v_j>, <v_j,b>
+        } else if (sl == 2) {
+            vi = 2 + j;          // <v_j,v_j>
+        }
+        if (vi >= 0) st(d.P1, (int64_t)vi * a.ntiles + slot, sum);
+    }
+}
+
 // W = U - alpha v_j (src/orthogonal_bases.jl:53);  P2 = [ <W,W> ]
 __global__ __launch_bounds__(TPB) void k_lan_l2(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
@@ -1589,6 +1672,16 @@ void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     const size_t lds = lds_bytes(1, a.kmax, 0);
     with_fmt(a.fmt, [&](auto FM) {
         hipLaunchKernelGGL((k_lan_l1_plain<decltype(FM)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
+    });
+}
+void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
+    const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
+    const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
+    with_fmt(a.fmt, [&](auto FM) {
+        with_maxc(a.j, [&](auto Mc) {
+            hipLaunchKernelGGL((k_lan_d1<decltype(Mc)::value, decltype(FM)::value>), grid, dim3(TPB), lds, s, F, a);
+        });
     });
 }
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
