@@ -222,7 +222,8 @@ def test_arnoldi_mid_run_flush(ctx, cls):
         assert np.array_equal(x, y) if exact else np.abs(x - y).max() <= 1e-12
 
 
-@pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20)])
+@pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20),
+                                     ("Laplace", 700, 75)])
 def test_lanczos_matches_oracle(ctx, cls, n, K):
     tk = _tk()
     csc = tk.assemble_matrix(n, cls)
@@ -341,3 +342,22 @@ def test_basis_mul_mfma(ctx):
             assert np.abs(X[f] - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
     dev.close()
     A.close()
+
+
+@pytest.mark.parametrize("n,K", [(3000, 30), (1000, 70)])
+def test_lanczos_untracked_factors_identical(ctx, n, K):
+    """Factors without a Gram row take k_lan_d1's light path (no register row): their H
+    entries, b-tilde and basis are bitwise those of the same factors stepped with Gram rows."""
+    tk = _tk()
+    csc = tk.assemble_matrix(n, "Laplace")
+    bs = _rhs(n, 3, 17, distinct=True)
+    ra, Va = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K, track_all=True)
+    rb, Vb = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K, track_all=False)
+    m = ra[0].shape[1]
+    kmax = (m - 10) // 2
+    keep = np.r_[0:kmax + 2, 2 * kmax + 4, 2 * kmax + 6]   # H column, b-tilde, beta
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x[:, keep], y[:, keep])
+    for x, y in zip(Va, Vb):
+        assert np.array_equal(x, y)
+
