@@ -618,6 +618,15 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #define TRACE_MAX 8192
 __device__ int g_trace_j = -1;
 __device__ uint64_t g_trace[3 * TRACE_MAX];
+__device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, SpMV 1, SpMV 2, dots)
+#define D1_PHASE(k)                                                                   \
+    do {                                                                              \
+        __builtin_amdgcn_s_waitcnt(0);                                                \
+        if (t == 0 && blockIdx.y == 0 && j == g_trace_j && slot < TRACE_MAX)          \
+            g_trace_ph[4 * slot + (k)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+#else
+#define D1_PHASE(k) do { } while (0)
 #endif
 template <int MAXC, int FMT>
 #ifndef TK_D1_OCCT
@@ -698,6 +707,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #else
         row_dot2<MAXC>(R, c, h1, sc, sh);
 #endif
+        D1_PHASE(0);
         const double vj = ok ? (up - sc) * inv_beta : 0.0;
         double* xv = xs[par];
         double* xu = xs[2 + par];
@@ -705,9 +715,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         __syncthreads();
         const double av = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
         const double u = ok ? av - (sh + h1j * vj) : 0.0;
+        D1_PHASE(1);
         xu[t] = u;
         __syncthreads();
         const double z = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xu[clamp_row(cc - S)]; }) : 0.0;
+        D1_PHASE(2);
         const bool own = ok && t >= 2 * hl && t < TPB - 2 * hu;
         if (own) {
             st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, (j & 1) ? R.last : 0.0);
@@ -749,6 +761,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     }
     // combine the 16 row-group partials of every value (fixed order) -> P1
     //   [ p (c<j) | q (c<j) | p_j, q_j, |u|^2, <u,z>, <v_j,v_0>, gram_jj | gram (c<j) ]
+    D1_PHASE(3);
     __syncthreads();
     for (int e = t; e < nch * 16; e += TPB) {
         const int k = e >> 4, sl = e & 15;
@@ -1746,6 +1759,9 @@ void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, doubl
 extern "C" int tk_debug_d1_trace(int j, uint64_t* out, int n) {
     if (!out) return (int)hipMemcpyToSymbol(HIP_SYMBOL(tk::g_trace_j), &j, sizeof(int));
     hipDeviceSynchronize();
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tk::g_trace), sizeof(uint64_t) * 3 * (n < TRACE_MAX ? n : TRACE_MAX));
+    const int m = n < TRACE_MAX ? n : TRACE_MAX;
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(tk::g_trace), sizeof(uint64_t) * 3 * m);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(out + 3 * m, HIP_SYMBOL(tk::g_trace_ph), sizeof(uint64_t) * 4 * m);
+    return (int)e;
 }
 #endif

@@ -38,10 +38,12 @@ def main():
             dev.sweep(0, K)
             dev.flush(False)
             ctx.sync()
-        buf = np.zeros(3 * 8192, dtype=np.uint64)
+        buf = np.zeros(7 * 8192, dtype=np.uint64)
         fn(-1, buf.ctypes.data, 8192)
-        tr = buf.reshape(-1, 3)
-        tr = tr[tr[:, 0] > 0]
+        tr = buf[:3 * 8192].reshape(-1, 3)
+        ph = buf[3 * 8192:].reshape(-1, 4)
+        keep = tr[:, 0] > 0
+        tr, ph = tr[keep], ph[keep]
         t0 = tr[:, 0].min()
         st = (tr[:, 0] - t0).astype(np.float64) / 100.0    # us (100 MHz)
         en = (tr[:, 1] - t0).astype(np.float64) / 100.0
@@ -52,6 +54,10 @@ def main():
         se = (hw >> 13) & 0x7
         print("j=%d blocks %d span %.2f us  dur p10/50/90/max %.2f %.2f %.2f %.2f  first-end %.2f  last-start %.2f"
               % (j, len(tr), en.max(), *np.percentile(du, [10, 50, 90]), du.max(), en.min(), st.max()))
+        if ph[:, 3].min() > 0:   # phase clocks: median time from block start to each phase
+            rel = (ph.astype(np.float64) - tr[:, :1].astype(np.float64)) / 100.0
+            print("  phases (median us from block start): loads %.2f  spmv1 %.2f  spmv2 %.2f  dots %.2f  end %.2f"
+                  % (*np.median(rel, axis=0), np.median(du)))
         grid = np.arange(0, en.max() + 1.0, 1.0)
         act = [int(((st <= g) & (en > g)).sum()) for g in grid]
         print("  active blocks per us:", " ".join(str(a) for a in act))
