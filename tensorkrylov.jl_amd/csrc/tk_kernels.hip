@@ -130,6 +130,45 @@ __device__ __forceinline__ double rs16(const double (&x)[16]) {
     return (b0 ? w[1] : w[0]) + dpp<0xB1>(b0 ? w[0] : w[1]);
 }
 
+// Reduce-scatter over the whole wave: lane l returns the sum over all 64 lanes of
+// x[(l >> 2) & 15] (lanes 4v..4v+3 hold value v, bitwise equal).  The two cross-row steps
+// are v_permlane32_swap / v_permlane16_swap half exchanges (gfx950): with vdst = the half the
+// lower rows keep and src = the half the upper rows keep, one swap per dword leaves every
+// lane with its own and its partner's copy of the half it keeps -- no select.  Then
+// row_ror:8 and row_half_mirror halve the last four values (as rs16) and two quad_perm
+// all-reduce steps finish.  Fixed order; 63 VALU per 16 values against rs16's 105.
+__device__ __forceinline__ double swap_add32(double a, double b) {   // lanes < 32: a, else b
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    const double na = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    const double nb = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+    return na + nb;
+}
+__device__ __forceinline__ double swap_add16(double a, double b) {   // even rows: a, odd: b
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    const double na = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    const double nb = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+    return na + nb;
+}
+__device__ __forceinline__ double rs64(const double (&x)[16]) {
+    const int l = threadIdx.x & 15;
+    const bool b3 = l & 8, b2 = l & 4;
+    double y[8], z[4], w[2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y[i] = swap_add32(x[i], x[8 + i]);   // value i + 8 [lane >= 32]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = swap_add16(y[i], y[4 + i]);   // + 4 [odd row]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) w[i] = (b3 ? z[2 + i] : z[i]) + dpp<0x128>(b3 ? z[i] : z[2 + i]);
+    double s = (b2 ? w[1] : w[0]) + dpp<0x141>(b2 ? w[0] : w[1]);
+    s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
+    s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
+    return s;
+}
+
 // Accumulate CH per-thread values x[0..CH) over the block's 256 rows into
 // acc[base .. base+CH) (LDS).  Fixed order: lane (col*16+part) sums rows q*16+part of
 // column col (q ascending), then a DPP row sum.
@@ -611,6 +650,24 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 // combined once, after the last window.  Chunk k < NUZ holds columns 8k..8k+7 times
 // (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row (16 columns
 // each).  acc[chunk][256]: slot t = (16-row group p = t >> 4, value s = t & 15).
+// Column-dot accumulation of k_arn_d1: rs64 (whole-wave reduce-scatter; the 16 values of a
+// chunk land in 4 wave slots) or rs16 (16-lane rows; 16 row-group slots per chunk)
+#ifndef TK_D1_RS64
+#define TK_D1_RS64 1
+#endif
+#if TK_D1_RS64
+#define D1_ACC(k, x)                                                                    \
+    do {                                                                                \
+        const double r_ = rs64(x);                                                      \
+        if ((t & 3) == 0) acc[(k) * 64 + (t >> 6) * 16 + ((t >> 2) & 15)] += r_;        \
+    } while (0)
+#define D1_NP 4
+#define D1_PART(k, p, sl) acc[(k) * 64 + (p) * 16 + (sl)]
+#else
+#define D1_ACC(k, x) acc[(k) * TPB + t] += rs16(x)
+#define D1_NP 16
+#define D1_PART(k, p, sl) acc[(k) * TPB + (p) * 16 + (sl)]
+#endif
 #if TK_D1_TRACE
 // diagnostic builds only (tools/build_variant.sh NAME - -DTK_D1_TRACE=1, tools/d1_trace.py):
 // per-block start / end wall clock (100 MHz) and HW_ID / XCC_ID of one step's k_arn_d1
@@ -739,7 +796,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                     x[2 * i] = R.v[8 * k + i] * uo;
                     x[2 * i + 1] = R.v[8 * k + i] * zo;
                 }
-                acc[k * TPB + t] += rs16(x);
+                D1_ACC(k, x);
             }
         }
         if (gram) {
@@ -749,14 +806,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                     double x[16];
 #pragma unroll
                     for (int i = 0; i < 16; ++i) x[i] = 16 * k + i < MAXC ? R.v[16 * k + i < MAXC ? 16 * k + i : 0] * vo : 0.0;
-                    acc[(NUZ + 1 + k) * TPB + t] += rs16(x);
+                    D1_ACC(NUZ + 1 + k, x);
                 }
             }
         }
 #endif
         {
             double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
-            acc[NUZ * TPB + t] += rs16(x);
+            D1_ACC(NUZ, x);
         }
     }
     // combine the 16 row-group partials of every value (fixed order) -> P1
@@ -767,7 +824,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         const int k = e >> 4, sl = e & 15;
         double sum = 0.0;
 #pragma unroll
-        for (int p = 0; p < 16; ++p) sum += acc[k * TPB + p * 16 + sl];
+        for (int p = 0; p < D1_NP; ++p) sum += D1_PART(k, p, sl);
         int vi = -1;
         if (k < NUZ) {
             const int col = 8 * k + (sl >> 1);
