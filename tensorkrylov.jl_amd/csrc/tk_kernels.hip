@@ -636,7 +636,7 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 // occupancy by register-row width (measured at C2: 4 waves/SIMD up to 32 columns, 3 up
 // to 56; 40 columns at 4 waves spill)
 #ifndef TK_D1_L4
-#define TK_D1_L4 32
+#define TK_D1_L4 40
 #endif
 #ifndef TK_D1_L3
 #define TK_D1_L3 56
@@ -687,11 +687,15 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #endif
 template <int MAXC, int FMT>
 #ifndef TK_D1_OCCT
-#define TK_D1_OCCT 1
+#define TK_D1_OCCT 2
 #endif
 #if TK_D1_OCCT
 // narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
+#if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows
+#define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 16 ? 6 : (MAXC <= 24 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3))))
+#else
 #define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
+#endif
 #else
 #define D1_OCC OCC_WAVES(TK_D1_L4, TK_D1_L3)
 #endif
