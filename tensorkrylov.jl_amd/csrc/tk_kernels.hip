@@ -153,6 +153,29 @@ __device__ __forceinline__ double swap_add16(double a, double b) {   // even row
     const double nb = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
     return na + nb;
 }
+// The half exchange itself: vd = (lanes < 32: a, else the partner's b), vs = (lanes < 32:
+// the partner's a, else b).
+__device__ __forceinline__ void swap32(double a, double b, double& vd, double& vs) {
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    vd = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    vs = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+}
+// rs64 after its first (cross-half) step: y[i] holds value i + 8 [lane >= 32]
+__device__ __forceinline__ double rs64_tail(const double (&y)[8]) {
+    const int l = threadIdx.x & 15;
+    const bool b3 = l & 8, b2 = l & 4;
+    double z[4], w[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[i] = swap_add16(y[i], y[4 + i]);   // + 4 [odd row]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) w[i] = (b3 ? z[2 + i] : z[i]) + dpp<0x128>(b3 ? z[i] : z[2 + i]);
+    double s = (b2 ? w[1] : w[0]) + dpp<0x141>(b2 ? w[0] : w[1]);
+    s += dpp<0x4E>(s);   // quad_perm [2,3,0,1]
+    s += dpp<0xB1>(s);   // quad_perm [1,0,3,2]
+    return s;
+}
 __device__ __forceinline__ double rs64(const double (&x)[16]) {
     const int l = threadIdx.x & 15;
     const bool b3 = l & 8, b2 = l & 4;
@@ -655,6 +678,14 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_RS64
 #define TK_D1_RS64 1
 #endif
+#ifndef TK_D1_SWPIN
+#define TK_D1_SWPIN 1
+#endif
+#define D1_ACC_Y(k, y)                                                                  \
+    do {                                                                                \
+        const double r_ = rs64_tail(y);                                                 \
+        if ((t & 3) == 0) acc[(k) * 64 + (t >> 6) * 16 + ((t >> 2) & 15)] += r_;        \
+    } while (0)
 #if TK_D1_RS64
 #define D1_ACC(k, x)                                                                    \
     do {                                                                                \
@@ -791,6 +822,40 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // 112-118): v_0 is column 0 of the register row, so b is not read (-8 B per row)
         const double v0r = j > 0 ? R.v[0] : vj;
 #ifndef TK_D1_NORED   // (timing experiment: column dots skipped)
+#if TK_D1_RS64 && TK_D1_SWPIN
+        // rs64's first step on the inputs: the basis entries of columns c and c+4 are
+        // half-exchanged once for the u, the z and the Gram products, and each lane forms its
+        // half's two-lane sums as one product and one FMA (the partner's u, z, v come from one
+        // exchange per window).  Gram chunk g takes the pairs of column chunks 2g and 2g+1.
+        double mu1, mu2, mz1, mz2, mv1 = 0.0, mv2 = 0.0;
+        swap32(uo, uo, mu1, mu2);
+        swap32(zo, zo, mz1, mz2);
+        if (gram) swap32(vo, vo, mv1, mv2);
+#pragma unroll
+        for (int g = 0; g < (NUZ + 1) / 2; ++g) {
+            double yg[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = 2 * g + h;
+                if (k < NUZ && 8 * k < j) {
+                    double y[8];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        double vd, vs;
+                        swap32(R.v[8 * k + q], R.v[8 * k + 4 + q], vd, vs);
+                        y[2 * q] = fma(vs, mu2, vd * mu1);
+                        y[2 * q + 1] = fma(vs, mz2, vd * mz1);
+                        yg[4 * h + q] = gram ? fma(vs, mv2, vd * mv1) : 0.0;
+                    }
+                    D1_ACC_Y(k, y);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) yg[4 * h + q] = 0.0;
+                }
+            }
+            if (gram && 16 * g < j) D1_ACC_Y(NUZ + 1 + g, yg);
+        }
+#else
 #pragma unroll
         for (int k = 0; k < NUZ; ++k) {
             if (8 * k < j) {
@@ -815,6 +880,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             }
         }
 #endif
+#endif
         {
             double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
             D1_ACC(NUZ, x);
@@ -836,7 +902,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         } else if (k == NUZ) {
             if (sl < 6) vi = 2 * j + sl;
         } else {
+#if TK_D1_RS64 && TK_D1_SWPIN   // slot sl of Gram chunk g: pair q = sl & 3 of column chunk
+                                // 2g + bit 2, upper column (+4) for bit 3
+            const int col = 16 * (k - NUZ - 1) + (sl & 3) + 8 * ((sl >> 2) & 1) + 4 * ((sl >> 3) & 1);
+#else
             const int col = 16 * (k - NUZ - 1) + sl;
+#endif
             if (col < j) vi = 2 * j + 6 + col;
         }
         if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
