@@ -845,7 +845,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                         swap32(R.v[8 * k + q], R.v[8 * k + 4 + q], vd, vs);
                         y[2 * q] = fma(vs, mu2, vd * mu1);
                         y[2 * q + 1] = fma(vs, mz2, vd * mz1);
-                        yg[4 * h + q] = gram ? fma(vs, mv2, vd * mv1) : 0.0;
+                        yg[4 * h + q] = fma(vs, mv2, vd * mv1);   // 0 unless gram (mv = 0)
                     }
                     D1_ACC_Y(k, y);
                 } else {
@@ -882,8 +882,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
 #endif
         {
+#if TK_D1_RS64 && TK_D1_SWPIN
+            // the six scalars in value slots 0..2 (lower half-wave) and 8..10 (upper): three
+            // cross-half exchanges, the rest of the first step is zeros
+            double y[8] = {swap_add32(vo * u, uo * z), swap_add32(vo * z, vo * v0r), swap_add32(uo * u, vo * vj)};
+            D1_ACC_Y(NUZ, y);
+#else
             double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
             D1_ACC(NUZ, x);
+#endif
         }
     }
     // combine the 16 row-group partials of every value (fixed order) -> P1
@@ -900,7 +907,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             const int col = 8 * k + (sl >> 1);
             if (col < j) vi = (sl & 1) ? j + col : col;
         } else if (k == NUZ) {
+#if TK_D1_RS64 && TK_D1_SWPIN
+            if ((sl & 7) < 3) vi = 2 * j + (sl < 8 ? sl : sl - 5);   // slots 0,1,2 | 8,9,10
+#else
             if (sl < 6) vi = 2 * j + sl;
+#endif
         } else {
 #if TK_D1_RS64 && TK_D1_SWPIN   // slot sl of Gram chunk g: pair q = sl & 3 of column chunk
                                 // 2g + bit 2, upper column (+4) for bit 3
