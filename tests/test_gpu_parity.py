@@ -361,3 +361,24 @@ def test_lanczos_untracked_factors_identical(ctx, n, K):
     for x, y in zip(Va, Vb):
         assert np.array_equal(x, y)
 
+
+@pytest.mark.parametrize("orth", ["auto", "cgs2"])
+def test_arnoldi_untracked_factors_identical(ctx, orth, monkeypatch):
+    """Factors without a Gram row skip the Gram products (one-sweep: the Gram chunks share the
+    column-pair exchanges of the u/z dots): their H columns, b-tilde and basis are bitwise
+    those of the same factors stepped with Gram rows."""
+    _orth_env(orth, monkeypatch)
+    tk = _tk()
+    n, K = 3000, 40
+    csc = tk.assemble_matrix(n, "ConvDiff")
+    bs = _rhs(n, 3, 23, distinct=True)
+    ra, Va = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, track_all=True)
+    rb, Vb = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, track_all=False)
+    m = ra[0].shape[1]
+    kmax = (m - 10) // 2
+    keep = np.r_[0:kmax + 2, 2 * kmax + 4, 2 * kmax + 6]   # H column, b-tilde, beta
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x[:, keep], y[:, keep])
+    for x, y in zip(Va, Vb):
+        assert np.array_equal(x, y)
+
