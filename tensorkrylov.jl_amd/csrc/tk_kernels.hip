@@ -1412,17 +1412,26 @@ __device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* H
     // every global load of the kernel in one round trip: Hbar[:, 0..j) (16 per thread in
     // flight; j <= 64 fits), the reduced dots, the current h1 and norm(b).  The record row is
     // assembled in LDS (row) and written out once.
-    for (int i0 = 0; i0 < j * J2; i0 += 16 * TPB) {
-        double hv[16];
+    // (a wave per column, a lane per row: no index division; columns i, i+4, ... of a wave
+    // in flight together)
+    {
+        const int w = t >> 6, ln = t & 63;
+        for (int l0 = 0; l0 < J2; l0 += 64) {
+            const int l = l0 + ln;
+            for (int i0 = 0; i0 < j; i0 += 64) {
+                double hv[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int idx = i0 + q * TPB + t;
-            const int i = idx / J2, l = idx - i * J2;
-            hv[q] = (idx < j * J2 && l <= i + 1) ? ld(d.H, (int64_t)i * (kmax + 2) + l) : 0.0;
+                for (int q = 0; q < 16; ++q) {
+                    const int i = i0 + 4 * q + w;
+                    hv[q] = (i < j && l <= i + 1) ? ld(d.H, (int64_t)i * (kmax + 2) + l) : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int i = i0 + 4 * q + w;
+                    if (i < j && l < J2) Hs[i * J2 + l] = hv[q];
+                }
+            }
         }
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if (i0 + q * TPB + t < j * J2) Hs[i0 + q * TPB + t] = hv[q];
     }
     for (int i = t; i < nv; i += TPB) red[i] = ld(d.RED1, i);
     for (int i = t; i <= j; i += TPB) h1s[i] = ld(d.g, i);
