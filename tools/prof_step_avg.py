@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Average duration of one Arnoldi factor-step launch group (pass 1 + reduce + pass 2 +
-reduce + post, all local factors) from a rocprofv3 --kernel-trace --stats summary, for
+reduce + post, or the one-sweep k_arn_d1 + reduce + post; all local factors) from a rocprofv3 --kernel-trace --stats summary, for
 comparison with bench.py's live HIP-event figure (roofline.avg_launch_us).
 
 usage: prof_step_avg.py KERNEL_STATS.csv SWEEPS K
@@ -8,7 +8,7 @@ usage: prof_step_avg.py KERNEL_STATS.csv SWEEPS K
 import csv
 import sys
 
-STEP = ("k_arn_a1", "k_arn_a2", "k_reduce", "k_post")
+STEP = ("k_arn_a1", "k_arn_a2", "k_arn_d1", "k_reduce", "k_post")
 
 
 def main():
