@@ -78,7 +78,8 @@ def main():
     ap.add_argument("--method", default=None, choices=["TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"],
                     help="orthonormalization type (default: the config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU work per baseline mode (1 core, all cores)")
     ap.add_argument("--force-comm", action="store_true",
                     help="1 rank: still build an RCCL communicator and route every step's records "
                          "through the all-reduce on the exchange stream (the N>1 code path)")
@@ -362,12 +363,19 @@ def exchange_uid(tkamd, rank, timeout=120.0):
 
 
 def cpu_baseline(csc, n, d, K, seconds):
-    """The C restatement's K-step Arnoldi sweeps timed on one host core, on a bounded
-    sample of the workload's factors (oracle/tk_ref.py baseline())."""
+    """The C restatement's K-step Arnoldi (MGS2) sweeps on a bounded sample of the
+    workload's factors: on one host core (oracle/tk_ref.py baseline(): the reference's
+    effective concurrency -- its factor loop runs one task at a time) and with the rows
+    split over all the cores OpenMP is given (baseline_all_cores(): the reference with a
+    threaded BLAS).  `value`/`cores` are the 1-core figure; `all_cores` the other; the
+    host's CPU model and core counts are reported beside them."""
     try:
         sys.path.insert(0, ROOT)
         from oracle import tk_ref
-        return tk_ref.baseline(csc, n, d, K, seconds)
+        one = tk_ref.baseline(csc, n, d, K, seconds)
+        one["all_cores"] = tk_ref.baseline_all_cores(csc, n, d, K, seconds)
+        one.update(tk_ref.cpu_info())
+        return one
     except Exception as e:   # noqa: BLE001
         return {"value": None, "unit": "iterations/s", "cores": None, "kind": "port",
                 "sample": "unavailable: %s" % e}

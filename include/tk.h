@@ -45,7 +45,8 @@ enum {
     TK_ERR_STATE = 4,    /* call out of sequence (e.g. step j != next step)   */
     TK_ERR_RCCL = 5,     /* RCCL error                                         */
     TK_ERR_NODEV = 6,    /* no usable gfx950 device                            */
-    TK_BREAKDOWN = 7     /* compressed norm breakdown (src/utils.jl:7-14, :395)  */
+    TK_BREAKDOWN = 7,    /* compressed norm breakdown (src/utils.jl:7-14, :395)  */
+    TK_ERR_INTERNAL = 8  /* unexpected host-side exception, caught at the boundary */
 };
 
 /* Orthonormalization types: src/decompositions.jl:120-176 (TensorArnoldi,
@@ -131,7 +132,11 @@ int tk_decomp_exchange_signalled(tk_decomp* dc);
 /* Per-factor record layout (doubles; m = tk_record_len(kmax)), written by every step:
  *   [0 .. kmax+1]        H[0..j+1, j] as computed by this step (rest 0)
  *   [kmax+2 .. 2kmax+3]  Gram row G[c, 0..c] = V[:,c]' V[:,0..c] of column c below
- *   [2kmax+4]            btilde[c] = <V[:,c], b_s>   (update_rhs!, src/utils.jl:466-476)
+ *   [2kmax+4]            btilde[c] = <V[:,c], b_s>   (update_rhs!, src/utils.jl:466-476).
+ *                        One-sweep Arnoldi handles (tk_decomp_arnoldi_sweeps == 1) form it
+ *                        as norm(b_s) * <V[:,c], V[:,0]> (b_s = norm(b_s) V[:,0], so b_s is
+ *                        not re-read); the other paths dot with b_s itself.  Equal in exact
+ *                        arithmetic; they round differently (both O(eps) for c > 0).
  *   [2kmax+5]            c (column of the Gram row / btilde entry), -1 if none
  *   [2kmax+6]            beta = H[j+1, j] (after any re-orthogonalization)
  *   [2kmax+7]            loss (LanczosReorth: ||V[:,0..j+1]'V[:,0..j+1] - I||_F after TTR)

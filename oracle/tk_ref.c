@@ -91,3 +91,74 @@ void tkref_lanczos_step(int64_t n, const int64_t* colptr, const int64_t* rowval,
     *alpha_out = alpha;
     *beta_out = beta;
 }
+
+/* ------------------------------------------------------------------ all-cores baseline
+ * The same K-step MGS2 sweep (src/orthogonal_bases.jl:15-37) with the rows split over
+ * OpenMP threads -- what the reference's dot/axpy would run with a threaded BLAS
+ * (test/tensor_krylov_method.jl:33 sets BLAS.set_num_threads(30)).  SpMV as CSR row sums
+ * (each row's products added in ascending column order, bitwise the CSC scatter); every
+ * MGS projection: per-thread partial dot, one barrier, every thread sums the partials in
+ * thread order; the axpy of projection i is fused with the partial dot of projection i+1.
+ * Only the dot reduction order differs from tkref_arnoldi_step (results equal to rounding).
+ * V column-major (ldv), H column-major (ldh), V[:,0] = b/|b| on entry. */
+#include <omp.h>
+void tkref_arnoldi_sweep_omp(int64_t n, const int64_t* rowptr, const int64_t* colind, const double* val,
+                             double* V, int64_t ldv, double* H, int64_t ldh, int K, double* w,
+                             int nthreads, double* partial /* 2 * 8 * nthreads */) {
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+    {
+        const int nt = omp_get_num_threads(), t = omp_get_thread_num();
+        const int64_t r0 = n * t / nt, r1 = n * (t + 1) / nt;
+        int buf = 0;
+#define TK_PART(b, th) partial[((b) * nt + (th)) * 8]
+#define TK_SUM(res)                                                   \
+    do {                                                              \
+        _Pragma("omp barrier");                                       \
+        double s_ = 0.0;                                              \
+        for (int q_ = 0; q_ < nt; ++q_) s_ += TK_PART(buf, q_);       \
+        (res) = s_;                                                   \
+        buf ^= 1;                                                     \
+    } while (0)
+        for (int j = 0; j < K; ++j) {
+            const double* vj = V + (int64_t)j * ldv;
+            double* Hc = H + (int64_t)j * ldh;
+            double acc = 0.0;
+            for (int64_t r = r0; r < r1; ++r) {           /* w = A v_j ; partial <w, v_0> */
+                double y = 0.0;
+                for (int64_t p = rowptr[r]; p < rowptr[r + 1]; ++p) y += val[p] * vj[colind[p]];
+                w[r] = y;
+                acc += y * V[r];
+            }
+            TK_PART(buf, t) = acc;
+            for (int pass = 0; pass < 2; ++pass)
+                for (int i = 0; i <= j; ++i) {
+                    double h;
+                    TK_SUM(h);
+                    if (t == 0) Hc[i] = pass == 0 ? h : Hc[i] + h;
+                    const double* vi = V + (int64_t)i * ldv;
+                    const int last = pass == 1 && i == j;
+                    const double* vn = last ? w : (i < j ? vi + ldv : V);  /* next projection's column */
+                    acc = 0.0;
+                    for (int64_t r = r0; r < r1; ++r) {
+                        const double x = w[r] - h * vi[r];
+                        w[r] = x;
+                        acc += x * (last ? x : vn[r]);
+                    }
+                    TK_PART(buf, t) = acc;
+                }
+            double nrm2;
+            TK_SUM(nrm2);
+            const double nrm = sqrt(nrm2);
+            if (t == 0) Hc[j + 1] = nrm;
+            const double inv = 1.0 / nrm;
+            double* vnew = V + (int64_t)(j + 1) * ldv;
+            for (int64_t r = r0; r < r1; ++r) vnew[r] = w[r] * inv;
+#pragma omp barrier
+        }
+#undef TK_SUM
+#undef TK_PART
+    }
+}
+
+int tkref_max_threads(void) { return omp_get_max_threads(); }

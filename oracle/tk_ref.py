@@ -32,6 +32,9 @@ def lib():
                                          ctypes.c_int64, ctypes.c_int, D]
         L.tkref_lanczos_step.argtypes = [ctypes.c_int64, I64, I64, D, D, ctypes.c_int64, ctypes.c_int,
                                          ctypes.c_double, D, D, D]
+        L.tkref_arnoldi_sweep_omp.argtypes = [ctypes.c_int64, I64, I64, D, D, ctypes.c_int64, D,
+                                              ctypes.c_int64, ctypes.c_int, D, ctypes.c_int, D]
+        L.tkref_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -108,3 +111,80 @@ def baseline(csc, n, d, K, seconds=15.0):
             "sample": "oracle/tk_ref.c MGS2 Arnoldi, full K=%d sweeps of %d factor(s) of the workload "
                       "(n=%d; d=%d), %.1f s of CPU work, mean sweep x d" % (K, len(sweeps), n, d,
                                                                          float(np.sum(sweeps)))}
+
+
+def csc_to_csr(csc):
+    """Row-major copy of a CSC matrix with every row's columns ascending (the order the CSC
+    scatter adds them in)."""
+    colptr, rowval, nz = (np.asarray(a) for a in csc)
+    n = len(colptr) - 1
+    cols = np.repeat(np.arange(n, dtype=np.int64), np.diff(colptr))
+    order = np.lexsort((cols, rowval))
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.bincount(rowval, minlength=n), out=rowptr[1:])
+    return rowptr, np.ascontiguousarray(cols[order]), np.ascontiguousarray(nz[order], dtype=np.float64)
+
+
+def arnoldi_sweep_omp(csr, b, K, threads=None, V=None, H=None):
+    """K-step MGS2 sweep with rows split over `threads` OpenMP threads (all-cores baseline);
+    returns V (n x K+1, Fortran order) and H ((K+2) x (K+1))."""
+    L = lib()
+    rowptr, colind, val = csr
+    n = len(rowptr) - 1
+    threads = threads or L.tkref_max_threads()
+    if V is None:
+        V = np.zeros((n, K + 1), order="F")
+    if H is None:
+        H = np.zeros((K + 2, K + 1), order="F")
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    L.tkref_init(n, _d(b), _d(V))
+    w = np.zeros(n)
+    part = np.zeros(2 * 8 * threads)
+    L.tkref_arnoldi_sweep_omp(n, _i(rowptr), _i(colind), _d(val), _d(V), n, _d(H), H.shape[0], int(K),
+                              _d(w), int(threads), _d(part))
+    return V, H
+
+
+def cpu_info():
+    """Host CPU model and the core count visible to this process."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": avail}
+
+
+def baseline_all_cores(csc, n, d, K, seconds=10.0, threads=None):
+    """All-cores CPU baseline: the MGS2 sweep with rows over OpenMP threads (threads =
+    OMP_NUM_THREADS / the OpenMP default), same factors and sampling rule as baseline()."""
+    threads = threads or lib().tkref_max_threads()
+    csr = csc_to_csr(csc)
+    V = np.zeros((n, K + 1), order="F")
+    H = np.zeros((K + 2, K + 1), order="F")
+    sweeps = []
+    s = 0
+    t_start = time.perf_counter()
+    while True:
+        rng = np.random.default_rng(1000 + (s % d))
+        b = rng.random(n)
+        b /= np.linalg.norm(b)
+        t0 = time.perf_counter()
+        arnoldi_sweep_omp(csr, b, K, threads, V, H)
+        sweeps.append(time.perf_counter() - t0)
+        s += 1
+        if time.perf_counter() - t_start >= seconds or s >= 4 * d:
+            break
+    per_iter = d * float(np.mean(sweeps)) / K
+    return {"value": round(1.0 / per_iter, 4), "unit": "iterations/s", "cores": int(threads), "kind": "port",
+            "sample": "oracle/tk_ref.c MGS2 Arnoldi, rows over %d OpenMP threads, full K=%d sweeps of %d "
+                      "factor(s) of the workload (n=%d; d=%d), %.1f s, mean sweep x d"
+                      % (threads, K, len(sweeps), n, d, float(np.sum(sweeps)))}

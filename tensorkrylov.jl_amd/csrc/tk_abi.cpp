@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <exception>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -21,17 +23,28 @@
 using namespace tk;
 
 // ------------------------------------------------------------------ errors
-static thread_local std::string g_err;
+// a fixed buffer: recording an error never allocates (a bad_alloc is itself reported here)
+static thread_local char g_err[1024];
 
 static tk_status fail(int code, const char* fmt, ...) {
-    char buf[1024];
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
-    g_err = buf;
     return code;
 }
+
+// tk_host.cpp reports through the same thread-local message
+tk_status tk_fail_internal(int code, const char* msg) { return fail(code, "%s", msg); }
+
+// Every exported body runs inside TK_API_BEGIN / TK_API_END: host containers (std::vector)
+// may throw, and tk.h promises that nothing throws across the ABI.
+#define TK_API_BEGIN try {
+#define TK_API_END                                                                        \
+    }                                                                                     \
+    catch (const std::bad_alloc&) { return fail(TK_ERR_ALLOC, "host allocation failed"); } \
+    catch (const std::exception& ex_) { return fail(TK_ERR_INTERNAL, "%s", ex_.what()); } \
+    catch (...) { return fail(TK_ERR_INTERNAL, "unknown C++ exception"); }
 
 #define HIPCHK(x)                                                                         \
     do {                                                                                  \
@@ -126,10 +139,10 @@ static void drain_timers(tk_ctx* c) {
 
 extern "C" {
 
-const char* tk_last_error(void) { return g_err.c_str(); }
+const char* tk_last_error(void) { return g_err; }
 int tk_version(void) { return 100; }
 
-tk_status tk_ctx_create(int device, tk_ctx** out) {
+tk_status tk_ctx_create(int device, tk_ctx** out) { TK_API_BEGIN
     CHECKARG(out, "out is NULL");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TK_ERR_NODEV, "no HIP device visible");
@@ -149,6 +162,7 @@ tk_status tk_ctx_create(int device, tk_ctx** out) {
     }
     *out = c;
     return TK_OK;
+    TK_API_END
 }
 
 static void ctx_release(tk_ctx* c) {
@@ -165,30 +179,33 @@ static void ctx_release(tk_ctx* c) {
     delete c;
 }
 
-tk_status tk_ctx_destroy(tk_ctx* c) {
+tk_status tk_ctx_destroy(tk_ctx* c) { TK_API_BEGIN
     if (!c) return TK_OK;
     ctx_release(c);
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_ctx_sync(tk_ctx* c) {
+tk_status tk_ctx_sync(tk_ctx* c) { TK_API_BEGIN
     CHECKARG(c, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->xstream));
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_comm_unique_id(char id_out[128]) {
+tk_status tk_comm_unique_id(char id_out[128]) { TK_API_BEGIN
     CHECKARG(id_out, "id_out is NULL");
     ncclUniqueId id;
     NCCLCHK(ncclGetUniqueId(&id));
     static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
     memcpy(id_out, &id, 128);
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_comm_init(tk_ctx* c, const char id[128], int nranks, int rank) {
+tk_status tk_comm_init(tk_ctx* c, const char id[128], int nranks, int rank) { TK_API_BEGIN
     CHECKARG(c && id, "NULL argument");
     CHECKARG(nranks >= 1 && rank >= 0 && rank < nranks, "bad nranks/rank");
     HIPCHK(hipSetDevice(c->device));
@@ -198,9 +215,10 @@ tk_status tk_comm_init(tk_ctx* c, const char id[128], int nranks, int rank) {
     c->nranks = nranks;
     c->rank = rank;
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) {
+tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_BEGIN
     CHECKARG(c && buf, "NULL argument");
     if (!c->comm || c->nranks == 1) return TK_OK;
     HIPCHK(hipSetDevice(c->device));
@@ -216,6 +234,7 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) {
     HIPCHK(hipMemcpyAsync(buf, c->xbuf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return TK_OK;
+    TK_API_END
 }
 
 // ------------------------------------------------------------------ matrices
@@ -289,6 +308,9 @@ static void build_dia(int64_t n, const std::vector<int>& rp, const std::vector<i
     std::vector<int> seen;
     for (int64_t r = 0; r < n; ++r)
         for (int p = rp[r]; p < rp[r + 1]; ++p) {
+            // a duplicate (row, column) entry of a non-canonical CSC: the scatter mul! adds
+            // both products in turn, which CSR/SELL reproduce bitwise and one DIA slot cannot
+            if (p > rp[r] && ci[p] == ci[p - 1]) return;
             const int o = ci[p] - (int)r;
             if (std::find(seen.begin(), seen.end(), o) == seen.end()) {
                 seen.push_back(o);
@@ -428,7 +450,7 @@ static tk_status upload_csr(tk_ctx* c, int64_t n, const std::vector<int>& rp, co
 }
 
 tk_status tk_matrix_from_csc(tk_ctx* c, int64_t n, const int64_t* colptr, const int64_t* rowval,
-                             const double* nzval, int one_based, tk_mat** out) {
+                             const double* nzval, int one_based, tk_mat** out) { TK_API_BEGIN
     CHECKARG(c && colptr && out && n > 0, "bad argument");
     const int64_t base = one_based ? 1 : 0;
     const int64_t nnz = colptr[n] - colptr[0];
@@ -456,10 +478,11 @@ tk_status tk_matrix_from_csc(tk_ctx* c, int64_t n, const int64_t* colptr, const 
         }
     }
     return upload_csr(c, n, rp, ci, v, out);
+    TK_API_END
 }
 
 tk_status tk_matrix_from_csr(tk_ctx* c, int64_t n, const int64_t* rowptr, const int64_t* colind,
-                             const double* val, int one_based, tk_mat** out) {
+                             const double* val, int one_based, tk_mat** out) { TK_API_BEGIN
     CHECKARG(c && rowptr && out && n > 0, "bad argument");
     const int64_t base = one_based ? 1 : 0;
     const int64_t nnz = rowptr[n] - rowptr[0];
@@ -479,6 +502,7 @@ tk_status tk_matrix_from_csr(tk_ctx* c, int64_t n, const int64_t* rowptr, const 
         }
     }
     return upload_csr(c, n, rp, ci, v, out);
+    TK_API_END
 }
 
 static void mat_release(tk_mat* A) {
@@ -490,15 +514,16 @@ static void mat_release(tk_mat* A) {
     ctx_release(c);
 }
 
-tk_status tk_matrix_destroy(tk_mat* A) {
+tk_status tk_matrix_destroy(tk_mat* A) { TK_API_BEGIN
     if (!A) return TK_OK;
     mat_release(A);
     return TK_OK;
+    TK_API_END
 }
 
 int tk_matrix_format(tk_mat* A) { return A ? (A->ndiag > 0 ? A->ndiag : (A->sell ? -2 : 0)) : -1; }
 
-tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
+tk_status tk_matvec(tk_mat* A, const double* x, double* y) { TK_API_BEGIN
     CHECKARG(A && x && y, "NULL argument");
     tk_ctx* c = A->ctx;
     HIPCHK(hipSetDevice(c->device));
@@ -516,6 +541,7 @@ tk_status tk_matvec(tk_mat* A, const double* x, double* y) {
     hipFree(dy);
     if (e != hipSuccess) return fail(TK_ERR_HIP, "tk_matvec: %s", hipGetErrorString(e));
     return TK_OK;
+    TK_API_END
 }
 
 // ------------------------------------------------------------------ decomposition
@@ -532,6 +558,8 @@ struct tk_decomp {
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
     bool in_sweep = false;  // inside tk_decomp_sweep: one timing pair for the whole sweep
+    bool failed = false;    // a step returned an error: later steps are refused
+    int fail_step = -1;     // TKHIP_TEST_FAIL_STEP=j at create: step j reports an error (tests)
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
@@ -585,7 +613,7 @@ static void free_decomp(tk_decomp* dc) {
 
 tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,
                            tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
-                           int track_all_gram, tk_decomp** out) {
+                           int track_all_gram, tk_decomp** out) { TK_API_BEGIN
     CHECKARG(c && mats && b && out, "NULL argument");
     CHECKARG(method >= TK_ARNOLDI && method <= TK_LANCZOS_REORTH, "unknown method");
     CHECKARG(nf >= 1 && d_total >= 1 && first_factor >= 0 && first_factor + nf <= d_total, "bad factor range");
@@ -694,6 +722,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
+    if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
     if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1')))
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
@@ -760,6 +789,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     for (tk_mat* A : dc->mats) A->refs++;
     *out = dc;
     return TK_OK;
+    TK_API_END
 }
 
 int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
@@ -769,7 +799,7 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
     return dc->onesweep ? 1 : 2;
 }
 
-tk_status tk_decomp_destroy(tk_decomp* dc) {
+tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     if (!dc) return TK_OK;
     tk_ctx* c = dc->ctx;
     std::vector<tk_mat*> mats = dc->mats;
@@ -780,6 +810,7 @@ tk_status tk_decomp_destroy(tk_decomp* dc) {
     for (tk_mat* A : mats) mat_release(A);
     ctx_release(c);
     return TK_OK;
+    TK_API_END
 }
 
 // Before a slot's send rows are rewritten, the previous all-reduce of that slot must
@@ -860,7 +891,7 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
     } while (0);                           \
     LAUNCHCHK(name)
 
-tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
+tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
@@ -886,6 +917,7 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) {
     dc->pending = false;
     dc->last_j = -1;
     return exchange_and_copy(dc, 0, rec_out);
+    TK_API_END
 }
 
 // write the pending column (Arnoldi / Lanczos fused pipeline)
@@ -1017,21 +1049,29 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     return TK_OK;
 }
 
-tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
+tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
+    if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
     if (!dc->inited) return fail(TK_ERR_STATE, "tk_decomp_init not called");
     if (j != dc->jnext) return fail(TK_ERR_STATE, "step %d requested, next step is %d", j, dc->jnext);
     if (j >= dc->kmax) return fail(TK_ERR_ARG, "step %d >= kmax %d", j, dc->kmax);
     HIPCHK(hipSetDevice(dc->ctx->device));
     const bool sig = dc->xflag != nullptr;
+    tk_status st = j == dc->fail_step ? fail(TK_ERR_HIP, "step %d: injected failure (TKHIP_TEST_FAIL_STEP)", j)
+                                      : step_impl(dc, j, rec_out);
+    if (st) {
+        // the exchange stream only ever waits for signal counts of steps that were fully
+        // enqueued, so a failed step cannot leave it blocked (destroy stays safe)
+        dc->failed = true;
+        return st;
+    }
     if (sig) dc->xcount += (unsigned long long)dc->nf;   // the step's k_post adds one per factor
-    tk_status st = step_impl(dc, j, rec_out);
-    if (st) return st;
     if (dc->hdone) dc->slot_seq[j + 1] = dc->seq;
     return exchange_and_copy(dc, j + 1, rec_out, sig);
+    TK_API_END
 }
 
-tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
+tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
     // one event pair brackets the whole sweep (events between the steps would idle the
     // GPU for their fences and inflate the very time they measure)
@@ -1041,10 +1081,12 @@ tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) {
     for (int j = j0; j < j1 && st == TK_OK; ++j) st = tk_decomp_step(dc, j, nullptr);
     dc->in_sweep = false;
     return st;
+    TK_API_END
 }
 
-tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {
+tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
+    if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
     HIPCHK(hipSetDevice(dc->ctx->device));
     const int slot = dc->kmax + 1;
     if (!dc->pending) {
@@ -1062,9 +1104,10 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) {
     if (st) return st;
     dc->pending = false;
     return exchange_and_copy(dc, slot, rec_out);
+    TK_API_END
 }
 
-tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
+tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API_BEGIN
     CHECKARG(dc && out, "NULL argument");
     CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
     HIPCHK(hipSetDevice(dc->ctx->device));
@@ -1109,9 +1152,10 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
                           dc->ctx->stream));
     HIPCHK(hipStreamSynchronize(dc->ctx->stream));
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out) {
+tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out) { TK_API_BEGIN
     CHECKARG(dc && out, "NULL argument");
     CHECKARG(f >= 0 && f < dc->nf, "factor out of range");
     CHECKARG(c0 >= 0 && nc >= 0 && c0 + nc <= dc->kmax + 1, "column range");
@@ -1137,9 +1181,10 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
                          hipMemcpyDeviceToHost));
     }
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X) {
+tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X) { TK_API_BEGIN
     CHECKARG(dc && Y, "NULL argument");
     CHECKARG(k >= 1 && k <= dc->kmax + 1 && t >= 1, "bad k/t");
     tk_ctx* c = dc->ctx;
@@ -1173,9 +1218,10 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
                                dc->n * sizeof(double), t, hipMemcpyDeviceToHost));
     }
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_timing_enable(tk_ctx* c, int on) {
+tk_status tk_timing_enable(tk_ctx* c, int on) { TK_API_BEGIN
     CHECKARG(c, "NULL ctx");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1186,9 +1232,10 @@ tk_status tk_timing_enable(tk_ctx* c, int on) {
     }
     c->timing = on;
     return TK_OK;
+    TK_API_END
 }
 
-tk_status tk_timing_read(tk_ctx* c, int cls, double* total_ms, long* launches) {
+tk_status tk_timing_read(tk_ctx* c, int cls, double* total_ms, long* launches) { TK_API_BEGIN
     CHECKARG(c && total_ms && launches, "NULL argument");
     CHECKARG(cls >= 0 && cls < TCLS_N, "timing class out of range");
     HIPCHK(hipSetDevice(c->device));
@@ -1196,6 +1243,7 @@ tk_status tk_timing_read(tk_ctx* c, int cls, double* total_ms, long* launches) {
     *total_ms = c->ms[cls];
     *launches = c->cnt[cls];
     return TK_OK;
+    TK_API_END
 }
 
 }  // extern "C"

@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <vector>
 
 #include "../../include/tk.h"
@@ -318,10 +319,19 @@ static bool expm(int n, const double* A, Vec& E) {
 
 using namespace tkh;
 
+tk_status tk_fail_internal(int code, const char* msg);   // tk_abi.cpp: tk_last_error()'s store
+
+// nothing throws across the ABI (include/tk.h): host containers' exceptions become statuses
+#define TK_API_BEGIN try {
+#define TK_API_END                                                                            \
+    }                                                                                         \
+    catch (const std::bad_alloc&) { return tk_fail_internal(TK_ERR_ALLOC, "host allocation failed"); } \
+    catch (...) { return tk_fail_internal(TK_ERR_INTERNAL, "unknown C++ exception"); }
+
 extern "C" {
 
 tk_status tk_compressed_solve(int d, int k, const double* H1, int symmetric, const double* bt, int t,
-                              const double* alpha, const double* omega, double lmin, double* lambda, double* Y) {
+                              const double* alpha, const double* omega, double lmin, double* lambda, double* Y) { TK_API_BEGIN
     if (d < 1 || k < 1 || t < 1 || !H1 || !bt || !alpha || !omega || !lambda || !Y) return TK_ERR_ARG;
     const double inv = 1.0 / lmin;                                    // src/utils.jl:507
     for (int j = 0; j < t; ++j) lambda[j] = inv * omega[j];
@@ -368,10 +378,11 @@ tk_status tk_compressed_solve(int d, int k, const double* H1, int symmetric, con
         }
     }
     return TK_OK;
+    TK_API_END
 }
 
 tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* lambda, const double* Y,
-                          const double* subdiag, const double* bt, double bnorm, double* r_comp, double* r_norm) {
+                          const double* subdiag, const double* bt, double bnorm, double* r_comp, double* r_norm) { TK_API_BEGIN
     if (d < 1 || k < 1 || t < 1 || !H || !lambda || !Y || !subdiag || !bt || !r_comp || !r_norm) return TK_ERR_ARG;
     const size_t tt = (size_t)t * t, kt = (size_t)k * t;
     auto y = [&](int s, int i, int j) { return Y[(size_t)s * kt + (size_t)j * k + i]; };
@@ -475,6 +486,7 @@ tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* la
     }
     *r_norm = sqrt(res + rc);
     return TK_OK;
+    TK_API_END
 }
 
 }  // extern "C"

@@ -59,11 +59,13 @@ def _pack(rows, vals, keep, n):
 
 
 def rand_sparse_spd(n, seed=42, nnz_row=15):
-    """Config C3 generator (defined by this build): each row draws
-    nnz_row-1 random off-diagonal columns with U(-1,0) values; A = (B + B')/2; diagonal
-    = sum |offdiag| + 1 (SPD by strict diagonal dominance).  Returns CSC (0-based)."""
+    """Config C3 generator (defined by this build; BASELINE.json configs[3]
+    "nnz/row ~ 15"): each row draws (nnz_row-1)//2 random off-diagonal columns with
+    U(-1,0) values; A = (B + B')/2 doubles them, so with the diagonal a row holds
+    ~nnz_row entries (14.99 at n = 2^19; duplicate draws are summed).  Diagonal =
+    sum |offdiag| + 1 (SPD by strict diagonal dominance).  Returns CSC (0-based)."""
     rng = np.random.default_rng(seed)
-    k = nnz_row - 1
+    k = (nnz_row - 1) // 2
     r = np.repeat(np.arange(n, dtype=np.int64), k)
     c = rng.integers(0, n - 1, size=n * k, dtype=np.int64)
     c = c + (c >= r)                        # skip the diagonal

@@ -1,0 +1,121 @@
+"""The C-ABI boundary from a non-Python caller, and its failure behaviour.
+
+  * tests/c/julia_glue_replay.c (built by __graft_entry__.build()) replays the Julia drop-in's
+    ccall sequence with the glue's literal 1-based record offsets
+    (julia/TensorKrylovHIP.jl:84-105, 227-255): the H, b-tilde and Gram rows it assembles
+    must equal the Python mirror's (tkamd.decompositions) bit for bit -- same library, same
+    kernels, so any difference is an offset or sequencing error in one of the two callers.
+  * a duplicate (row, column) entry in a non-canonical CSC is added like Julia's scatter
+    mul! (both products in turn), never stored over (the DIA format is refused for it).
+  * a failing step marks the handle failed instead of leaving the records exchange waiting
+    for a signal that never comes: later steps are refused and destroy returns.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from oracle import tk_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPLAY = os.path.join(ROOT, "tests", "c", "_build", "julia_glue_replay")
+
+
+def _tk():
+    import tkamd
+    return tkamd
+
+
+@pytest.mark.parametrize("method", ["TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"])
+def test_c_caller_replays_julia_glue(ctx, method, tmp_path):
+    tk = _tk()
+    code = {"TensorArnoldi": 0, "TensorLanczos": 1, "TensorLanczosReorth": 2}[method]
+    d, n, K = 3, 5000, 30
+    rng = np.random.default_rng(404)
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    rhs = tmp_path / "rhs.bin"
+    np.concatenate(bs).tofile(rhs)
+    out = tmp_path / "out.bin"
+    assert os.path.exists(REPLAY), "build() did not produce %s" % REPLAY
+    r = subprocess.run([REPLAY, str(code), str(d), str(n), str(K), str(rhs), str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    raw = np.fromfile(out, dtype=np.float64)
+    per = (K + 2) ** 2 + (K + 1) + (K + 1) ** 2
+    assert raw.size == d * per
+
+    csc = tk.assemble_matrix(n, "Laplace")
+    A = tk.KroneckerMatrix(tk.SymInstance, [csc] * d, tk.Laplace)
+    td = {"TensorArnoldi": tk.TensorArnoldi, "TensorLanczos": tk.TensorLanczos,
+          "TensorLanczosReorth": tk.TensorLanczosReorth}[method](A, K, ctx=ctx)
+    td.orthonormalize_first([b.copy() for b in bs])
+    for k in range(2, K + 1):
+        td.orthonormalize(k)
+    for s in range(d):
+        blk = raw[s * per:(s + 1) * per]
+        Hj = blk[:(K + 2) ** 2].reshape(K + 2, K + 2, order="F")
+        btj = blk[(K + 2) ** 2:(K + 2) ** 2 + K + 1]
+        Gj = blk[(K + 2) ** 2 + K + 1:].reshape(K + 1, K + 1, order="F")
+        # the glue's H is (kmax+2)^2; its last column is never written
+        assert np.array_equal(Hj[:, :K + 1], td.H[s]), (method, s)
+        assert not Hj[:, K + 1].any()
+        # b-tilde of columns 0..K-1 (column K is written by the flush neither caller ran)
+        assert np.array_equal(btj[:K], td.btilde[s, :K]), (method, s)
+        if s in td.gram:
+            assert np.array_equal(Gj[:K, :K], td.gram[s][:K, :K]), (method, s)
+        else:
+            assert not Gj.any()
+    assert 0 in td.gram                       # factor 1's Gram rows (orthogonality_data)
+    td.close()
+
+
+def test_duplicate_csc_entries_are_summed_like_the_scatter(ctx):
+    """A[0,0] given as two entries 1.5 + 0.5 of a tridiagonal matrix: Julia's mul! adds
+    nz1*x + nz2*x in turn; the device must not pick DIA (one slot per position)."""
+    tk = _tk()
+    n = 300
+    colptr, rowval, nz = tk.assemble_matrix(n, "Laplace")
+    nz = nz / nz.max()
+    # split the (0, 0) entry (column 0's second stored entry is row 1)
+    rowval = np.concatenate([[0, 0], rowval[1:]])
+    nz = np.concatenate([[nz[0] * 0.75, nz[0] * 0.25], nz[1:]])
+    colptr = colptr.copy()
+    colptr[1:] += 1
+    csc = (colptr, rowval, nz)
+    A = tk.DeviceMatrix(ctx, csc)
+    assert A.format <= 0                       # not DIA
+    x = np.random.default_rng(3).standard_normal(n)
+    assert np.array_equal(A.matvec(x), O.csc_matvec(csc, x))
+    A.close()
+
+
+def test_failed_step_refuses_later_steps_and_destroys(ctx, monkeypatch):
+    """Step 3 reports an injected error on a handle that routes its records through the RCCL
+    exchange (1-rank communicator): step 4 and flush are refused with TK_ERR_STATE and
+    destroy returns (no exchange left waiting for the failed step's signal)."""
+    tk = _tk()
+    n, K, d = 3000, 10, 2
+    csc = tk.assemble_matrix(n, "Laplace")
+    rng = np.random.default_rng(9)
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_TEST_FAIL_STEP", "3")
+    A = tk.DeviceMatrix(c2, csc)
+    dev = tk.DeviceDecomposition(c2, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+    dev.init()
+    for j in range(3):
+        dev.step(j)
+    with pytest.raises(tk.TKError, match="injected"):
+        dev.step(3)
+    with pytest.raises(tk.TKError, match="earlier step"):
+        dev.step(4)
+    with pytest.raises(tk.TKError, match="earlier step"):
+        dev.flush()
+    dev.close()
+    A.close()
+    c2.close()

@@ -1,6 +1,7 @@
 """GPU parity at full size and on the edge cases, through the C ABI.
 
-  * n = 2^20 (BASELINE configs C1/C2 factor size), K = 50: the device's H, V and records
+  * n = 2^20 (BASELINE config C2's factor size; C1/C3/C4 sizes are in test_gpu_configs.py),
+    K = 50: the device's H, V and records
     against the C restatement (oracle/tk_ref.c, MGS2) on the same inputs, plus the
     size-independent properties (orthonormality from the device Gram rows, the Arnoldi
     relation A V_K = V_{K+1} Hbar_K).
@@ -37,7 +38,7 @@ def _unit(v):
 
 # ------------------------------------------------------------------ full size
 def test_full_size_arnoldi_vs_c_oracle(ctx):
-    """C1/C2 factor size n = 2^20, K = 50, two factors with distinct b_s."""
+    """C2 factor size n = 2^20, K = 50, two factors with distinct b_s."""
     from oracle import tk_ref
     tk = _tk()
     n, K = 1 << 20, 50

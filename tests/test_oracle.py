@@ -145,3 +145,25 @@ def test_c_and_numpy_restatements_agree():
         assert np.abs(fc.V - fo.V).max() <= 1e-12
         x = np.random.default_rng(3).standard_normal(300)
         assert np.array_equal(fc.matvec(x), O.csc_matvec(csc, x))
+
+
+def test_all_cores_baseline_sweep_matches_port():
+    """bench.py's all-cores CPU baseline (rows over OpenMP threads) computes the same MGS2
+    sweep as the 1-core port: only the dot reduction order differs (rounding level)."""
+    from oracle import tk_ref
+    import tkamd
+    n, K = 6000, 30
+    for cls in ("Laplace", "RandSparseSPD"):
+        csc = tkamd.assemble_matrix(n, cls)
+        b = np.random.default_rng(5).random(n)
+        b /= np.linalg.norm(b)
+        f = tk_ref.RefFactor(csc, b, K)
+        for j in range(K):
+            f.arnoldi_step(j)
+        csr = tk_ref.csc_to_csr(csc)
+        V1, H1 = tk_ref.arnoldi_sweep_omp(csr, b, K, threads=1)
+        assert np.array_equal(V1, f.V) and np.array_equal(H1[:K + 1, :K], f.H[:K + 1, :K])
+        V, H = tk_ref.arnoldi_sweep_omp(csr, b, K, threads=4)
+        scale = np.abs(f.H).max()
+        assert np.abs(H[:K + 1, :K] - f.H[:K + 1, :K]).max() <= 1e-12 * scale
+        assert np.abs(V - f.V).max() <= 1e-12
