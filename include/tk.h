@@ -212,6 +212,49 @@ tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* la
                           const double* subdiag, const double* bt, double bnorm, double* r_comp,
                           double* r_norm);
 
+/* ---------------------------------------------------------------- native iteration driver
+ * The host side of tensorkrylov!'s loop (src/tensor_krylov_method.jl:63-118) in native code:
+ * a tk_solver keeps the host mirror of H_s, b~_s and factor 1's Gram rows, applies step
+ * records exactly as the reference mutates H (orthonormalize!, update_subdiagonals!,
+ * LanczosReorth's zeroing, update_rhs!) and evaluates iteration k = compressed solve +
+ * residualnorm! + orthogonality_loss(V_1, k).  The spectral / exp-sum data depend only on
+ * A and tol and are passed per k at create: lmin[k-1] (lambda_min of the k x k minor times
+ * d, src/eigenvalues.jl:353-370), rank[k-1] = t (0 = no tabulated rank: the loop stops
+ * before k) and t coefficients alpha/omega per k, concatenated in k order
+ * (src/approximation.jl:65-175). */
+typedef struct tk_solver tk_solver;
+tk_status tk_solver_create(int method, int d, int kmax, int symmetric, double b_norm, const double* lmin,
+                           const int* rank, const double* alpha, const double* omega, tk_solver** out);
+tk_status tk_solver_destroy(tk_solver* sv);
+/* Apply the records [d][m] of ABI step j (j = -1: tk_decomp_init's record). */
+tk_status tk_solver_apply(tk_solver* sv, int j, const double* rec);
+/* Evaluate iteration k (records of steps < k applied): out4 = {r_comp, r_norm,
+ * r_norm / norm(b), orthogonality loss of V_1}.  TK_BREAKDOWN as tk_residualnorm. */
+tk_status tk_solver_evaluate(tk_solver* sv, int k, double* out4);
+int tk_solver_rank(tk_solver* sv, int k);
+/* lambda (t) and Y [d][t][k] of iteration k, which must be the last one evaluated (by
+ * tk_solver_evaluate, or the iteration tk_solver_run ended on). */
+tk_status tk_solver_solution(tk_solver* sv, int k, double* lambda_out, double* Y_out);
+/* Host mirror: H [d][kmax+2][kmax+1] (row-major), b~ [d][kmax+1], Gram rows of factor 1
+ * [(kmax+1)^2] (row c holds G[c, 0..c]); NULL outputs are skipped. */
+tk_status tk_solver_state(tk_solver* sv, double* H_out, double* bt_out, double* gram0_out);
+/* Diagnostic (bench.py --emulate-ranks): records of factors outside [first, first+nf) are
+ * replaced, whenever records are applied, by those of a full run, records[slot][d][m]
+ * (slot = j + 1, kmax + 2 slots), so one GPU holding one rank's factors drives the same
+ * iterates as the whole job.  records = NULL removes the overlay. */
+tk_status tk_solver_overlay(tk_solver* sv, int first, int nf, const double* records);
+/* The pipelined loop for k = kfirst .. kmax on a decomposition whose steps < kfirst-1 are
+ * done and applied: enqueues steps up to `depth` ahead, applies each step's records in
+ * order and evaluates up to `nthreads` iterations concurrently on host threads (each
+ * iteration's evaluation reads only data that later steps do not touch, so every iterate
+ * is bitwise the sequential loop's).  relres / projres / orth [kmax] receive the
+ * reference's ConvergenceData entries (index k-1).  *outcome: 0 = no convergence through
+ * *k_end, 1 = converged at *k_end (tk_solver_solution gives its y), 2 = compressed norm
+ * breakdown at *k_end + 1 (src/tensor_krylov_method.jl:83-95).  Steps enqueued beyond
+ * *k_end may still run; their results are not read. */
+tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, int depth, int nthreads,
+                        double* relres, double* projres, double* orth, int* k_end, int* outcome);
+
 #ifdef __cplusplus
 }
 #endif

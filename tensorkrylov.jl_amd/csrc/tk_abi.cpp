@@ -570,6 +570,10 @@ struct tk_decomp {
     unsigned long long* hdone = nullptr;    // [(kmax+2) slots][nf]
     unsigned long long seq = 0;
     std::vector<unsigned long long> slot_seq;   // per slot: seq of the signalled step that wrote it, 0 = none
+    // multi-rank: each exchanged slot is mirrored to hrec by the exchange stream, xdone[slot]
+    // = its sequence number (host-mapped); xslot_seq[slot] = the number to wait for
+    unsigned long long* xdone = nullptr;
+    std::vector<unsigned long long> xslot_seq;
     hipStream_t cstream = nullptr;          // record copies (multi-rank): no wait on the compute queue
     int last_j = -1;
     std::vector<tk_mat*> mats;
@@ -607,6 +611,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->hrec) hipHostFree(dc->hrec);
     if (dc->hdone) hipHostFree(dc->hdone);
+    if (dc->xdone) hipHostFree(dc->xdone);
     if (dc->cstream) hipStreamDestroy(dc->cstream);
     delete dc;
 }
@@ -780,9 +785,24 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
                 if (hr) hipHostFree(hr);
                 if (hd) hipHostFree(hd);
             }
-        } else if (hipStreamCreateWithFlags(&dc->cstream, hipStreamNonBlocking) != hipSuccess) {
-            dc->cstream = nullptr;
+        } else {
+            if (hipStreamCreateWithFlags(&dc->cstream, hipStreamNonBlocking) != hipSuccess) dc->cstream = nullptr;
+            void* hr = nullptr;
+            void* hd = nullptr;
+            const size_t nrec = (size_t)(kmax + 2) * d_total * dc->m;
+            if (hipHostMalloc(&hr, nrec * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+                hipHostMalloc(&hd, (size_t)(kmax + 2) * sizeof(unsigned long long),
+                              hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+                memset(hr, 0, nrec * sizeof(double));
+                memset(hd, 0, (size_t)(kmax + 2) * sizeof(unsigned long long));
+                dc->hrec = (double*)hr;
+                dc->xdone = (unsigned long long*)hd;
+            } else {
+                if (hr) hipHostFree(hr);
+                if (hd) hipHostFree(hd);
+            }
         }
+        dc->xslot_seq.assign(kmax + 2, 0);
         (void)hipGetLastError();
     }
     c->refs++;
@@ -865,6 +885,11 @@ static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out, boo
             NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->xstream));
         }
         HIPCHK(hipEventRecord(dc->ev_x[slot], c->xstream));
+        if (dc->xdone) {
+            dc->xslot_seq[slot] = ++dc->seq;
+            launch_mirror_records(r, dc->hrec + (size_t)slot * cnt, (int)cnt, dc->xdone + slot, dc->seq, c->xstream);
+            LAUNCHCHK("mirror_records");
+        }
         if (rec_out) {
             HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->xstream));
             HIPCHK(hipStreamSynchronize(c->xstream));
@@ -1132,6 +1157,26 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
                         if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)
                             return fail(TK_ERR_STATE, "step records of slot %d never arrived", sl);
                     }
+                }
+            }
+        }
+        memcpy(out, dc->hrec + (size_t)s0 * per, (s1 - s0) * per * sizeof(double));
+        return TK_OK;
+    }
+    bool xhosted = dc->xdone != nullptr;
+    for (int sl = s0; sl < s1 && xhosted; ++sl) xhosted = dc->xslot_seq[sl] != 0;
+    if (xhosted) {
+        // multi-rank: wait for the exchange stream's mirror of each slot (host-mapped words)
+        for (int sl = s0; sl < s1; ++sl) {
+            const unsigned long long want = dc->xslot_seq[sl];
+            long spins = 0;
+            while (__atomic_load_n(dc->xdone + sl, __ATOMIC_ACQUIRE) < want) {
+                if (++spins % 4096 == 0) {
+                    hipError_t e = hipStreamQuery(dc->ctx->xstream);
+                    if (e != hipSuccess && e != hipErrorNotReady)
+                        return fail(TK_ERR_HIP, "waiting for exchanged records: %s", hipGetErrorString(e));
+                    if (e == hipSuccess && __atomic_load_n(dc->xdone + sl, __ATOMIC_ACQUIRE) < want)
+                        return fail(TK_ERR_STATE, "exchanged records of slot %d never arrived", sl);
                 }
             }
         }

@@ -23,10 +23,9 @@
 #include <vector>
 
 #include "../../include/tk.h"
+#include "tk_host.h"
 
 namespace tkh {
-
-typedef std::vector<double> Vec;
 
 // ------------------------------------------------------------------ symmetric eigen
 // A (n x n, column-major, symmetric; only the lower triangle is read) -> eigenvalues w
@@ -92,6 +91,14 @@ static void tridiagonalize(int n, Vec& Q, Vec& diag, Vec& off) {
 #undef A_
 }
 
+// sqrt(a^2 + b^2) without libm's hypot (its overflow-safe scaling costs more than the rest
+// of a QL rotation); falls back to hypot outside the range where the squares are exact-safe
+static inline double fast_hypot(double a, double b) {
+    const double m = std::max(fabs(a), fabs(b));
+    if (m > 1e-150 && m < 1e150) return sqrt(a * a + b * b);
+    return hypot(a, b);
+}
+
 static bool tql(int n, Vec& d, Vec& e, Vec& Z) {
     // implicit QL on the tridiagonal (d, e[1..n-1]) accumulating into Z
     for (int i = 1; i < n; ++i) e[i - 1] = e[i];
@@ -106,14 +113,14 @@ static bool tql(int n, Vec& d, Vec& e, Vec& Z) {
             if (m != l) {
                 if (++iter > 60) return false;
                 double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-                double r = hypot(g, 1.0);
+                double r = fast_hypot(g, 1.0);
                 g = d[m] - d[l] + e[l] / (g + (g >= 0.0 ? fabs(r) : -fabs(r)));
                 double s = 1.0, c = 1.0, p = 0.0;
                 int i;
                 for (i = m - 1; i >= l; --i) {
                     double f = s * e[i];
                     const double b = c * e[i];
-                    e[i + 1] = (r = hypot(f, g));
+                    e[i + 1] = (r = fast_hypot(f, g));
                     if (r == 0.0) {
                         d[i + 1] -= p;
                         e[m] = 0.0;
@@ -125,10 +132,12 @@ static bool tql(int n, Vec& d, Vec& e, Vec& Z) {
                     r = (d[i] - g) * s + 2.0 * c * b;
                     d[i + 1] = g + (p = s * r);
                     g = c * r - b;
+                    double* __restrict zi = &Z[(size_t)i * n];
+                    double* __restrict zn = &Z[(size_t)(i + 1) * n];
                     for (int k = 0; k < n; ++k) {
-                        f = Z[(size_t)(i + 1) * n + k];
-                        Z[(size_t)(i + 1) * n + k] = s * Z[(size_t)i * n + k] + c * f;
-                        Z[(size_t)i * n + k] = c * Z[(size_t)i * n + k] - s * f;
+                        const double a = zi[k], b2 = zn[k];
+                        zn[k] = s * a + c * b2;
+                        zi[k] = c * a - s * b2;
                     }
                 }
                 if (r == 0.0 && i >= l) continue;
@@ -141,7 +150,7 @@ static bool tql(int n, Vec& d, Vec& e, Vec& Z) {
     return true;
 }
 
-static bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q) {
+bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q) {
     Q.assign((size_t)n * n, 0.0);
     // Symmetric(H, :L) of an upper-Hessenberg H (Arnoldi) or of a Lanczos T is already
     // tridiagonal: QL directly on (diag, subdiag), Q starting from the identity
@@ -229,7 +238,7 @@ static bool lu_solve(int n, Vec& A, Vec& B) {
 
 // exp(A) by Pade approximants of degree 3/5/7/9/13 with scaling and squaring (Higham 2005,
 // the method of Julia's LinearAlgebra.exp!)
-static bool expm(int n, const double* A, Vec& E) {
+bool expm(int n, const double* A, Vec& E) {
     static const double b13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
                                  1187353796428800.0,  129060195264000.0,   10559470521600.0,
                                  670442572800.0,      33522128640.0,       1323241920.0,
@@ -315,6 +324,242 @@ static bool expm(int n, const double* A, Vec& E) {
     return true;
 }
 
+
+// ------------------------------------------------------------------ compressed solve / residual
+// Dot product with four independent accumulators (vectorizable without reassociation flags).
+static inline double dot4(int n, const double* a, const double* b) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+        s0 += a[i] * b[i];
+        s1 += a[i + 1] * b[i + 1];
+        s2 += a[i + 2] * b[i + 2];
+        s3 += a[i + 3] * b[i + 3];
+    }
+    for (; i < n; ++i) s0 += a[i] * b[i];
+    return (s0 + s1) + (s2 + s3);
+}
+
+// C[0:m, 0:n] = A[0:m, 0:kk] * B[0:kk, 0:n] (column-major; lda, ldb, ldc); register blocks of
+// 8 rows x 4 columns, the inner dimension streamed (vectorized over rows).
+static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, const double* __restrict B, int ldb,
+                    double* __restrict C, int ldc) {
+    int j0 = 0;
+    for (; j0 + 4 <= n; j0 += 4) {
+        const double* b0 = B + (size_t)j0 * ldb;
+        int i0 = 0;
+        for (; i0 + 8 <= m; i0 += 8) {
+            double acc[4][8] = {};
+            for (int c = 0; c < kk; ++c) {
+                const double* a = A + (size_t)c * lda + i0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const double bv = b0[(size_t)q * ldb + c];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) acc[q][r] += a[r] * bv;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) C[(size_t)(j0 + q) * ldc + i0 + r] = acc[q][r];
+        }
+        for (; i0 < m; ++i0) {
+            double acc[4] = {};
+            for (int c = 0; c < kk; ++c) {
+                const double av = A[(size_t)c * lda + i0];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[q] += av * b0[(size_t)q * ldb + c];
+            }
+            for (int q = 0; q < 4; ++q) C[(size_t)(j0 + q) * ldc + i0] = acc[q];
+        }
+    }
+    for (; j0 < n; ++j0) {
+        const double* bj = B + (size_t)j0 * ldb;
+        double* cj = C + (size_t)j0 * ldc;
+        for (int i = 0; i < m; ++i) cj[i] = 0.0;
+        for (int c = 0; c < kk; ++c) {
+            const double* a = A + (size_t)c * lda;
+            const double bv = bj[c];
+            for (int i = 0; i < m; ++i) cj[i] += a[i] * bv;
+        }
+    }
+}
+
+// C[i, j] = <A[:, i], B[:, j]> for i < m, j < n (A: kk x m, B: kk x n, column-major, leading
+// dimension kk; C row-major with stride ldc) through row-major copies: rows of A' and B'
+// are broadcast against contiguous output rows.
+static void gemm_tn(int m, int n, int kk, const double* A, const double* B, double* C, int ldc, Vec& tmp) {
+    // Bt[r][j] = B[r, j]  (kk x n, row stride n)
+    tmp.resize((size_t)kk * n);
+    double* __restrict Bt = tmp.data();
+    for (int j = 0; j < n; ++j)
+        for (int r = 0; r < kk; ++r) Bt[(size_t)r * n + j] = B[(size_t)j * kk + r];
+    for (int i = 0; i < m; ++i) {
+        double* __restrict ci = C + (size_t)i * ldc;
+        for (int j = 0; j < n; ++j) ci[j] = 0.0;
+        const double* ai = A + (size_t)i * kk;
+        for (int r = 0; r < kk; ++r) {
+            const double av = ai[r];
+            const double* br = Bt + (size_t)r * n;
+            for (int j = 0; j < n; ++j) ci[j] += av * br[j];
+        }
+    }
+}
+
+bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, const double* bt, int ldb,
+                      int t, const double* alpha, const double* omega, double lmin, double* lambda, double* Y,
+                      Work& ws) {
+    const double inv = 1.0 / lmin;                                    // src/utils.jl:507
+    for (int j = 0; j < t; ++j) lambda[j] = inv * omega[j];
+    if (symmetric) {
+        // exp(g Symmetric(H1, :L)) = Q exp(g w) Q' for every term: one eigendecomposition
+        if (!sym_eig(k, H1, ldh, ws.w, ws.Q)) return false;
+        const double* Q = ws.Q.data();
+        ws.C.resize((size_t)k * d);
+        for (int s = 0; s < d; ++s)                                   // C = Q' B
+            for (int c = 0; c < k; ++c) ws.C[(size_t)s * k + c] = dot4(k, Q + (size_t)c * k, bt + (size_t)s * ldb);
+        ws.E.resize((size_t)k * t);
+        for (int j = 0; j < t; ++j) {
+            const double g = -alpha[j] * inv;
+            for (int c = 0; c < k; ++c) ws.E[(size_t)j * k + c] = exp(ws.w[c] * g);
+        }
+        // M[:, (s, j)] = exp(g_j w) .* C[:, s];  Y_s[:, j] = Q M[:, (s, j)]
+        ws.M.resize((size_t)k * t * d);
+        for (int s = 0; s < d; ++s)
+            for (int j = 0; j < t; ++j) {
+                double* m = &ws.M[((size_t)s * t + j) * k];
+                const double* e = &ws.E[(size_t)j * k];
+                const double* cs = &ws.C[(size_t)s * k];
+                for (int c = 0; c < k; ++c) m[c] = e[c] * cs[c];
+            }
+        gemm_nn(k, t * d, k, Q, k, ws.M.data(), k, Y, k);
+    } else {
+        ws.G.resize((size_t)k * k);
+        for (int j = 0; j < t; ++j) {
+            const double g = -alpha[j] * inv;
+            for (int c = 0; c < k; ++c)
+                for (int i = 0; i < k; ++i) ws.G[(size_t)c * k + i] = g * H1[(size_t)c * ldh + i];
+            if (!expm(k, ws.G.data(), ws.Ex)) return false;
+            for (int s = 0; s < d; ++s) {
+                double* y = Y + (size_t)s * k * t + (size_t)j * k;
+                for (int i = 0; i < k; ++i) y[i] = 0.0;
+                for (int c = 0; c < k; ++c) {
+                    const double b = bt[(size_t)s * ldb + c];
+                    const double* e = &ws.Ex[(size_t)c * k];
+                    for (int i = 0; i < k; ++i) y[i] += e[i] * b;
+                }
+            }
+        }
+    }
+    return true;
+}
+
+int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const double* lambda, const double* Y,
+             const double* subdiag, const double* bt, int ldb, double bnorm, double* r_comp, double* r_norm,
+             Work& ws) {
+    const size_t tt = (size_t)t * t, kt = (size_t)k * t;
+    auto y = [&](int s, int i, int j) { return Y[(size_t)s * kt + (size_t)j * k + i]; };
+    // Z_s = H_s Y_s;  Ly_s = lower(Y_s' Y_s), Lz_s = lower(Z_s' Z_s), X_s = Y_s' Z_s  ([i*t+j])
+    ws.Z.assign((size_t)d * kt, 0.0);
+    ws.Ly.assign(d * tt, 0.0);
+    ws.Lz.assign(d * tt, 0.0);
+    ws.X.assign(d * tt, 0.0);
+    ws.G.resize((size_t)4 * tt);
+    ws.M.resize((size_t)2 * kt);
+    for (int s = 0; s < d; ++s) {
+        const double* Hs = H + (size_t)s * hs;
+        double* Zs = &ws.Z[(size_t)s * kt];
+        const double* Ys = Y + (size_t)s * kt;
+        // (the minors are upper Hessenberg or tridiagonal; a dense GEMM in register blocks
+        // is still cheaper than a column-by-column band update)
+        gemm_nn(k, t, k, Hs, ldh, Ys, k, Zs, k);
+        // G = [Y Z]' [Y Z]  (2t x 2t, row-major): Ly = lower(G11), X = G12, Lz = lower(G22)
+        double* YZ = ws.M.data();
+        memcpy(YZ, Ys, kt * sizeof(double));
+        memcpy(YZ + kt, Zs, kt * sizeof(double));
+        gemm_tn(2 * t, 2 * t, k, YZ, YZ, ws.G.data(), 2 * t, ws.Ex);
+        double* Ly = &ws.Ly[s * tt];
+        double* Lz = &ws.Lz[s * tt];
+        double* X = &ws.X[s * tt];
+        const double* G = ws.G.data();
+        for (int i = 0; i < t; ++i)
+            for (int j = 0; j < t; ++j) {
+                X[(size_t)i * t + j] = G[(size_t)i * 2 * t + t + j];
+                if (j <= i) {
+                    Ly[(size_t)i * t + j] = G[(size_t)i * 2 * t + j];
+                    Lz[(size_t)i * t + j] = G[(size_t)(t + i) * 2 * t + t + j];
+                }
+            }
+    }
+    auto W = [&](int i, int j) { return i == j ? 1.0 : 2.0; };   // lower triangle only
+    // first term: sum_s beta_s^2 * sum W .* Gamma_s .* prod_{q != s} Ly_q  (prefix/suffix)
+    ws.pre.assign(d * tt, 1.0);
+    ws.suf.assign(d * tt, 1.0);
+    double* pre = ws.pre.data();
+    double* suf = ws.suf.data();
+    const double* Ly = ws.Ly.data();
+    const double* Lz = ws.Lz.data();
+    const double* X = ws.X.data();
+    for (int s = 1; s < d; ++s)
+        for (size_t e = 0; e < tt; ++e) pre[s * tt + e] = pre[(s - 1) * tt + e] * Ly[(s - 1) * tt + e];
+    for (int s = d - 2; s >= 0; --s)
+        for (size_t e = 0; e < tt; ++e) suf[s * tt + e] = suf[(s + 1) * tt + e] * Ly[(s + 1) * tt + e];
+    double res = 0.0;
+    for (int s = 0; s < d; ++s) {
+        double acc = 0.0;
+        for (int i = 0; i < t; ++i)
+            for (int j = 0; j <= i; ++j) {
+                const double gam = y(s, k - 1, i) * y(s, k - 1, j) * (lambda[i] * lambda[j]);
+                acc += W(i, j) * gam * (pre[s * tt + (size_t)i * t + j] * suf[s * tt + (size_t)i * t + j]);
+            }
+        res += subdiag[s] * subdiag[s] * acc;
+    }
+    // compressed residual ||Hy||^2: per element e = (i, j), j <= i,
+    //   sum_s Lz_s prod_{q != s} Ly_q + sum_{s != r} X_s[e] X_r[e'] prod_{q != s, r} Ly_q
+    // accumulated in one pass over the factors (states: no factor chosen, one Lz chosen,
+    // one X_s[e] / one X_r[e'] chosen, two chosen) -- O(d t^2) instead of O(d^3 t^2)
+    double hy_norm = 0.0;
+    for (int i = 0; i < t; ++i)
+        for (int j = 0; j <= i; ++j) {
+            const size_t e = (size_t)i * t + j, et = (size_t)j * t + i;
+            double s0 = 1.0, sl = 0.0, sa = 0.0, sb = 0.0, s2 = 0.0;
+            for (int q = 0; q < d; ++q) {
+                const double ly = Ly[q * tt + e], xe = X[q * tt + e], xt = X[q * tt + et];
+                s2 = s2 * ly + sa * xt + sb * xe;
+                sa = sa * ly + s0 * xe;
+                sb = sb * ly + s0 * xt;
+                sl = sl * ly + s0 * Lz[q * tt + e];
+                s0 = s0 * ly;
+            }
+            hy_norm += W(i, j) * (lambda[i] * lambda[j]) * (sl + s2);
+        }
+    // <Hy, b>: first rows of Y_s and Z_s
+    double hy_b = 0.0;
+    for (int j = 0; j < t; ++j)
+        for (int s = 0; s < d; ++s) {
+            double p = ws.Z[(size_t)s * kt + (size_t)j * k];
+            for (int q = 0; q < d; ++q)
+                if (q != s) p *= y(q, 0, j);
+            hy_b += lambda[j] * p;
+        }
+    hy_b *= bnorm;
+    double bn2 = 1.0;
+    for (int s = 0; s < d; ++s) {
+        double acc = 0.0;
+        for (int i = 0; i < k; ++i) acc += bt[(size_t)s * ldb + i] * bt[(size_t)s * ldb + i];
+        bn2 *= acc;
+    }
+    const double rc = hy_norm - 2 * hy_b + bn2;
+    *r_comp = rc;
+    if (rc < 0.0) {
+        *r_norm = NAN;
+        return 1;
+    }
+    *r_norm = sqrt(res + rc);
+    return 0;
+}
+
 }  // namespace tkh
 
 using namespace tkh;
@@ -333,50 +578,8 @@ extern "C" {
 tk_status tk_compressed_solve(int d, int k, const double* H1, int symmetric, const double* bt, int t,
                               const double* alpha, const double* omega, double lmin, double* lambda, double* Y) { TK_API_BEGIN
     if (d < 1 || k < 1 || t < 1 || !H1 || !bt || !alpha || !omega || !lambda || !Y) return TK_ERR_ARG;
-    const double inv = 1.0 / lmin;                                    // src/utils.jl:507
-    for (int j = 0; j < t; ++j) lambda[j] = inv * omega[j];
-    if (symmetric) {
-        Vec w, Q;
-        if (!sym_eig(k, H1, k, w, Q)) return TK_ERR_STATE;
-        // C = Q' B;  Y_s[:, j] = Q (exp(gamma_j w) .* C[:, s])
-        Vec C((size_t)k * d);
-        for (int s = 0; s < d; ++s)
-            for (int c = 0; c < k; ++c) {
-                double acc = 0.0;
-                for (int i = 0; i < k; ++i) acc += Q[(size_t)c * k + i] * bt[(size_t)s * k + i];
-                C[(size_t)s * k + c] = acc;
-            }
-        Vec ec(k);
-        for (int j = 0; j < t; ++j) {
-            const double g = -alpha[j] * inv;
-            for (int s = 0; s < d; ++s) {
-                for (int c = 0; c < k; ++c) ec[c] = exp(w[c] * g) * C[(size_t)s * k + c];
-                double* y = Y + (size_t)s * k * t + (size_t)j * k;
-                for (int i = 0; i < k; ++i) y[i] = 0.0;
-                for (int c = 0; c < k; ++c) {
-                    const double* q = &Q[(size_t)c * k];
-                    const double e = ec[c];
-                    for (int i = 0; i < k; ++i) y[i] += q[i] * e;
-                }
-            }
-        }
-    } else {
-        Vec G((size_t)k * k), E;
-        for (int j = 0; j < t; ++j) {
-            const double g = -alpha[j] * inv;
-            for (size_t i = 0; i < (size_t)k * k; ++i) G[i] = g * H1[i];
-            if (!expm(k, G.data(), E)) return TK_ERR_STATE;
-            for (int s = 0; s < d; ++s) {
-                double* y = Y + (size_t)s * k * t + (size_t)j * k;
-                for (int i = 0; i < k; ++i) y[i] = 0.0;
-                for (int c = 0; c < k; ++c) {
-                    const double b = bt[(size_t)s * k + c];
-                    const double* e = &E[(size_t)c * k];
-                    for (int i = 0; i < k; ++i) y[i] += e[i] * b;
-                }
-            }
-        }
-    }
+    Work ws;
+    if (!compressed_solve(d, k, H1, k, symmetric, bt, k, t, alpha, omega, lmin, lambda, Y, ws)) return TK_ERR_STATE;
     return TK_OK;
     TK_API_END
 }
@@ -384,108 +587,9 @@ tk_status tk_compressed_solve(int d, int k, const double* H1, int symmetric, con
 tk_status tk_residualnorm(int d, int k, int t, const double* H, const double* lambda, const double* Y,
                           const double* subdiag, const double* bt, double bnorm, double* r_comp, double* r_norm) { TK_API_BEGIN
     if (d < 1 || k < 1 || t < 1 || !H || !lambda || !Y || !subdiag || !bt || !r_comp || !r_norm) return TK_ERR_ARG;
-    const size_t tt = (size_t)t * t, kt = (size_t)k * t;
-    auto y = [&](int s, int i, int j) { return Y[(size_t)s * kt + (size_t)j * k + i]; };
-    // Ly_s = lower(Y_s' Y_s), Z_s = H_s Y_s, Lz_s = lower(Z_s' Z_s), X_s = Y_s' Z_s (t x t, [i*t+j])
-    Vec Ly(d * tt, 0.0), Lz(d * tt, 0.0), X(d * tt, 0.0), Z((size_t)d * kt, 0.0);
-    // rows of H below the first subdiagonal are zero for the Hessenberg / tridiagonal minors
-    // the driver passes (checked: a general H is handled too)
-    int band = 1;
-    for (int s = 0; s < d && band < k; ++s) {
-        const double* Hs = H + (size_t)s * k * k;
-        for (int b = 0; b < k; ++b)
-            for (int a = b + band + 1; a < k; ++a)
-                if (Hs[(size_t)b * k + a] != 0.0) band = a - b;
-    }
-    for (int s = 0; s < d; ++s) {
-        const double* Hs = H + (size_t)s * k * k;
-        double* Zs = &Z[(size_t)s * kt];
-        for (int j = 0; j < t; ++j)
-            for (int b = 0; b < k; ++b) {
-                const double yb = y(s, b, j);
-                const double* hc = Hs + (size_t)b * k;
-                const int amax = std::min(k, b + band + 1);
-                for (int a = 0; a < amax; ++a) Zs[(size_t)j * k + a] += hc[a] * yb;
-            }
-        for (int i = 0; i < t; ++i)
-            for (int j = 0; j < t; ++j) {
-                double sy = 0.0, sz = 0.0, sx = 0.0;
-                for (int r = 0; r < k; ++r) {
-                    sx += y(s, r, i) * Zs[(size_t)j * k + r];
-                    if (j <= i) {
-                        sy += y(s, r, i) * y(s, r, j);
-                        sz += Zs[(size_t)i * k + r] * Zs[(size_t)j * k + r];
-                    }
-                }
-                X[s * tt + (size_t)i * t + j] = sx;
-                if (j <= i) {
-                    Ly[s * tt + (size_t)i * t + j] = sy;
-                    Lz[s * tt + (size_t)i * t + j] = sz;
-                }
-            }
-    }
-    // prefix / suffix products of the Ly stack (elementwise)
-    Vec pre(d * tt, 1.0), suf(d * tt, 1.0);
-    for (int s = 1; s < d; ++s)
-        for (size_t e = 0; e < tt; ++e) pre[s * tt + e] = pre[(s - 1) * tt + e] * Ly[(s - 1) * tt + e];
-    for (int s = d - 2; s >= 0; --s)
-        for (size_t e = 0; e < tt; ++e) suf[s * tt + e] = suf[(s + 1) * tt + e] * Ly[(s + 1) * tt + e];
-    auto W = [&](int i, int j) { return i == j ? 1.0 : (j < i ? 2.0 : 0.0); };
-    // first term: sum_s beta_s^2 * sum W .* Gamma_s .* prod_{q != s} Ly_q
-    double res = 0.0;
-    for (int s = 0; s < d; ++s) {
-        double acc = 0.0;
-        for (int i = 0; i < t; ++i)
-            for (int j = 0; j <= i; ++j) {
-                const double gam = y(s, k - 1, i) * y(s, k - 1, j) * (lambda[i] * lambda[j]);
-                acc += W(i, j) * gam * (pre[s * tt + (size_t)i * t + j] * suf[s * tt + (size_t)i * t + j]);
-            }
-        res += subdiag[s] * subdiag[s] * acc;
-    }
-    // compressed residual: ||Hy||^2
-    Vec term(tt, 0.0), mid(tt);
-    for (int s = 0; s < d; ++s)
-        for (size_t e = 0; e < tt; ++e) term[e] += pre[s * tt + e] * suf[s * tt + e] * Lz[s * tt + e];
-    for (int s = 0; s < d; ++s)
-        for (int r = 0; r < d; ++r) {
-            if (r == s) continue;
-            const int a = std::min(s, r), b = std::max(s, r);
-            for (size_t e = 0; e < tt; ++e) mid[e] = 1.0;
-            for (int q = a + 1; q < b; ++q)
-                for (size_t e = 0; e < tt; ++e) mid[e] *= Ly[q * tt + e];
-            for (int i = 0; i < t; ++i)
-                for (int j = 0; j < t; ++j) {
-                    const size_t e = (size_t)i * t + j;
-                    term[e] += pre[a * tt + e] * mid[e] * suf[b * tt + e] * X[s * tt + e] * X[r * tt + (size_t)j * t + i];
-                }
-        }
-    double hy_norm = 0.0;
-    for (int i = 0; i < t; ++i)
-        for (int j = 0; j <= i; ++j) hy_norm += W(i, j) * (lambda[i] * lambda[j]) * term[(size_t)i * t + j];
-    // <Hy, b>: first rows of Y_s and Z_s
-    double hy_b = 0.0;
-    for (int j = 0; j < t; ++j)
-        for (int s = 0; s < d; ++s) {
-            double p = Z[(size_t)s * kt + (size_t)j * k];
-            for (int q = 0; q < d; ++q)
-                if (q != s) p *= y(q, 0, j);
-            hy_b += lambda[j] * p;
-        }
-    hy_b *= bnorm;
-    double bn2 = 1.0;
-    for (int s = 0; s < d; ++s) {
-        double acc = 0.0;
-        for (int i = 0; i < k; ++i) acc += bt[(size_t)s * k + i] * bt[(size_t)s * k + i];
-        bn2 *= acc;
-    }
-    const double rc = hy_norm - 2 * hy_b + bn2;
-    *r_comp = rc;
-    if (rc < 0.0) {
-        *r_norm = NAN;
-        return TK_BREAKDOWN;
-    }
-    *r_norm = sqrt(res + rc);
-    return TK_OK;
+    Work ws;
+    return residual(d, k, t, H, k, (size_t)k * k, lambda, Y, subdiag, bt, k, bnorm, r_comp, r_norm, ws)
+               ? TK_BREAKDOWN : TK_OK;
     TK_API_END
 }
 

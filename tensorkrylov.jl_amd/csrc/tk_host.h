@@ -1,0 +1,39 @@
+// tk_host.h -- host numerics shared by tk_host.cpp (compressed solve, residual) and
+// tk_solver.cpp (the native per-iteration driver).  Plain C++, no GPU.
+#pragma once
+#include <stddef.h>
+#include <vector>
+
+namespace tkh {
+
+typedef std::vector<double> Vec;
+
+// A (n x n column-major, leading dimension lda; lower triangle read) -> ascending
+// eigenvalues w and orthonormal eigenvectors Q (n x n column-major)
+bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q);
+// exp(A) (n x n column-major): Pade 3/5/7/9/13 with scaling and squaring
+bool expm(int n, const double* A, Vec& E);
+
+// Scratch of the two functions below (grown on demand, reused across iterations).
+struct Work {
+    Vec w, Q, C, E, M, ec, G, Ex;
+    Vec Z, Ly, Lz, X, pre, suf;
+};
+
+// solve_compressed_system (src/tensor_krylov_method.jl:10-34): lambda[j] = omega[j]/lmin and
+// Y_s[:, j] = exp(-alpha_j/lmin * first(H)) btilde_s for every factor s.
+//   H1: k x k (column-major, leading dimension ldh); bt: d vectors, stride ldb;
+//   Y: [s][j][i] (k x t column-major per factor).  false: eigen/expm failure.
+bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, const double* bt, int ldb,
+                      int t, const double* alpha, const double* omega, double lmin, double* lambda, double* Y,
+                      Work& ws);
+
+// residualnorm! + compressed_residual (src/utils.jl:371-443, Lemma 3.4).
+//   H: d minors k x k, column-major, leading dimension ldh, factor stride hs;
+//   Y: [s][j][i]; subdiag[s] = H_s[k+1, k]; bt: stride ldb.
+// Returns 0 (ok) or 1 (compressed norm breakdown: r_comp < 0, r_norm = NaN).
+int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const double* lambda, const double* Y,
+             const double* subdiag, const double* bt, int ldb, double bnorm, double* r_comp, double* r_norm,
+             Work& ws);
+
+}  // namespace tkh

@@ -1879,6 +1879,23 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
+// Multi-rank host mirror of one all-reduced record slot (runs on the exchange stream after
+// the all-reduce): copy the slot to host-mapped coherent memory, then publish its sequence
+// number, so the host reads the records without any queue call.
+__global__ __launch_bounds__(TPB) void k_mirror_records(const double* __restrict__ src, double* dst, int cnt,
+                                                        unsigned long long* done, unsigned long long seq) {
+    for (int i = threadIdx.x; i < cnt; i += TPB) dst[i] = ld(src, i);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, unsigned long long seq,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_mirror_records, dim3(1), dim3(TPB), 0, s, src, dst, cnt, done, seq);
+}
+
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
     size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;

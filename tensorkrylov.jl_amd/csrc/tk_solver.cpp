@@ -1,0 +1,436 @@
+// tk_solver.cpp -- the host side of tensorkrylov!'s iteration loop, native
+// (src/tensor_krylov_method.jl:63-118; SURVEY.md 8(b) "the C++ host driver", 8(f) rows 1-2).
+//
+// Per iteration k the reference's host work is: apply the step's results to H_s / b~_s
+// (orthonormalize! + update_rhs!), solve the compressed system, evaluate the residual, record
+// the orthogonality of V_1, test convergence.  Everything except the record bookkeeping is a
+// pure function of (H_s[1:k, 1:k], H_s[k+1, k], b~_s[1:k], the exp-sum table of k): steps
+// after k only write H columns >= k, rows >= k and b~ entries >= k.  So the driver
+// (tk_solver_run) applies records in order on the calling thread and hands each iteration's
+// evaluation to a pool of worker threads: iterations k, k+1, ... are evaluated concurrently
+// while the GPU runs further steps ahead, and results are consumed in order -- every
+// iterate is bitwise the one a sequential loop computes (the worker count changes only
+// throughput).  The spectral bounds and exp-sum ranks/coefficients depend on A and tol
+// only; the caller passes them per k (tk_solver_create).
+#include <math.h>
+#include <string.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <new>
+#include <thread>
+#include <vector>
+
+#include "../../include/tk.h"
+#include "tk_host.h"
+
+using namespace tkh;
+
+tk_status tk_fail_internal(int code, const char* msg);   // tk_abi.cpp: tk_last_error()'s store
+
+#define TK_API_BEGIN try {
+#define TK_API_END                                                                            \
+    }                                                                                         \
+    catch (const std::bad_alloc&) { return tk_fail_internal(TK_ERR_ALLOC, "host allocation failed"); } \
+    catch (...) { return tk_fail_internal(TK_ERR_INTERNAL, "unknown C++ exception"); }
+
+namespace {
+
+struct IterResult {
+    int k = 0;
+    int status = TK_OK;           // TK_OK, TK_BREAKDOWN or TK_ERR_STATE (eigen/expm failure)
+    double r_comp = 0.0, r_norm = 0.0, rel = 0.0, orth = 0.0;
+    Vec lam, Y;                   // lambda (t), Y [d][t][k]
+};
+
+}  // namespace
+
+struct tk_solver {
+    int method, d, kmax, KP, KC, m, symmetric;
+    double bnorm;
+    std::vector<double> lmin;
+    std::vector<int> rank, roff;
+    std::vector<double> alpha, omega;
+    std::vector<double> H;        // [s][c * KP + r]  (H_s, (kmax+2) x (kmax+1), column-major)
+    std::vector<double> bt;       // [s][c]
+    std::vector<double> gram0;    // factor 0's Gram rows: [c * KC + i], i <= c
+    std::vector<double> loss;     // [s][j] LanczosReorth loss of step j
+    std::vector<unsigned char> reorth;
+    IterResult last;
+    Work ws;
+    // emulation overlay (bench --emulate-ranks): rows of factors outside [ov_first,
+    // ov_first + ov_nf) are taken from records recorded by a full run, [slot][d][m]
+    std::vector<double> overlay;
+    int ov_first = 0, ov_nf = 0;
+};
+
+static void apply_record(tk_solver* sv, int j, const double* rec) {
+    const int kmax = sv->kmax, m = sv->m, KP = sv->KP, KC = sv->KC;
+    std::vector<double> merged;
+    if (!sv->overlay.empty()) {
+        merged.assign(rec, rec + (size_t)sv->d * m);
+        const double* ov = &sv->overlay[(size_t)(j + 1) * sv->d * m];
+        for (int s = 0; s < sv->d; ++s)
+            if (s < sv->ov_first || s >= sv->ov_first + sv->ov_nf)
+                memcpy(&merged[(size_t)s * m], ov + (size_t)s * m, m * sizeof(double));
+        rec = merged.data();
+    }
+    const int o_gram = kmax + 2, o_bt = 2 * kmax + 4, o_col = 2 * kmax + 5, o_loss = 2 * kmax + 7,
+              o_flag = 2 * kmax + 8, o_tracked = 2 * kmax + 9;
+    for (int s = 0; s < sv->d; ++s) {
+        const double* r = rec + (size_t)s * m;
+        double* H = &sv->H[(size_t)s * KP * KC];
+        auto h = [&](int row, int col) -> double& { return H[(size_t)col * KP + row]; };
+        if (j >= 0) {
+            if (sv->method == TK_ARNOLDI) {                       // H[:, j] (src/orthogonal_bases.jl:22-36)
+                for (int i = 0; i <= j + 1; ++i) h(i, j) = r[i];
+            } else {
+                double beta;
+                if (sv->method == TK_LANCZOS_REORTH) sv->loss[(size_t)s * KC + j] = r[o_loss];
+                if (sv->method == TK_LANCZOS_REORTH && r[o_flag] > 0) {   // :123-131
+                    sv->reorth[(size_t)s * KC + j] = 1;
+                    for (int i = 0; i <= j + 1; ++i) h(i, j) = r[i];
+                    beta = h(j + 1, j);
+                    for (int i = 0; i < std::max(j - 1, 0); ++i) h(i, j) = 0.0;
+                } else {                                          // TTR :50
+                    h(j, j) = r[j];
+                    beta = r[j + 1];
+                }
+                h(j + 1, j) = beta;                               // update_subdiagonals!
+                if (j + 1 < KC) h(j, j + 1) = beta;
+            }
+        }
+        const int c = (int)lround(r[o_col]);
+        if (c >= 0 && c < KC) {
+            sv->bt[(size_t)s * KC + c] = r[o_bt];                 // update_rhs! (src/utils.jl:466-476)
+            if (s == 0 && r[o_tracked] > 0)
+                for (int i = 0; i <= c; ++i) sv->gram0[(size_t)c * KC + i] = r[o_gram + i];
+        }
+    }
+}
+
+// iteration k (2 <= k <= kmax): compressed solve, residual, orthogonality of V_1
+static void evaluate(const tk_solver* sv, int k, IterResult& out, Work& ws) {
+    const int d = sv->d, KP = sv->KP, KC = sv->KC;
+    const int t = sv->rank[k - 1];
+    const double* al = &sv->alpha[sv->roff[k - 1]];
+    const double* om = &sv->omega[sv->roff[k - 1]];
+    out.k = k;
+    out.status = TK_OK;
+    out.lam.resize(t);
+    out.Y.resize((size_t)d * t * k);
+    if (!compressed_solve(d, k, sv->H.data(), KP, sv->symmetric, sv->bt.data(), KC, t, al, om, sv->lmin[k - 1],
+                          out.lam.data(), out.Y.data(), ws)) {
+        out.status = TK_ERR_STATE;
+        return;
+    }
+    double sub[64];
+    std::vector<double> subv;
+    double* sp = sub;
+    if (d > 64) {
+        subv.resize(d);
+        sp = subv.data();
+    }
+    for (int s = 0; s < d; ++s) sp[s] = sv->H[(size_t)s * KP * KC + (size_t)(k - 1) * KP + k];   // H_s[k+1, k]
+    if (residual(d, k, t, sv->H.data(), KP, (size_t)KP * KC, out.lam.data(), out.Y.data(), sp, sv->bt.data(), KC,
+                 sv->bnorm, &out.r_comp, &out.r_norm, ws)) {
+        out.status = TK_BREAKDOWN;
+        return;
+    }
+    out.rel = out.r_norm / sv->bnorm;                              // :99
+    // orthogonality_loss(V_1, k) = norm(V'V - I) from the lower Gram rows (:103)
+    double acc = 0.0;
+    for (int c = 0; c < k; ++c) {
+        const double* g = &sv->gram0[(size_t)c * KC];
+        const double dd = g[c] - 1.0;
+        double off = 0.0;
+        for (int i = 0; i < c; ++i) off += g[i] * g[i];
+        acc += dd * dd + 2.0 * off;
+    }
+    out.orth = sqrt(acc);
+}
+
+// ------------------------------------------------------------------ worker pool
+// Idle workers block (the box's CPU share is a cgroup quota: spinning threads would spend
+// it); a job is handed over under the worker's mutex, its completion under the pool's.
+namespace {
+
+struct Pool;
+
+struct Worker {
+    std::mutex mu;
+    std::condition_variable cv;
+    int job = 0;                  // iteration to evaluate, 0 = idle, -1 = exit
+    IterResult res;
+    Work ws;
+    std::thread th;
+};
+
+struct Pool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> done;        // per worker: iteration whose result is ready
+};
+
+}  // namespace
+
+extern "C" {
+
+tk_status tk_solver_create(int method, int d, int kmax, int symmetric, double b_norm, const double* lmin,
+                           const int* rank, const double* alpha, const double* omega, tk_solver** out) { TK_API_BEGIN
+    if (!out || d < 1 || kmax < 1 || !lmin || !rank || !alpha || !omega || method < 0 || method > 2)
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_create: bad argument");
+    tk_solver* sv = new tk_solver();
+    sv->method = method;
+    sv->d = d;
+    sv->kmax = kmax;
+    sv->KP = kmax + 2;
+    sv->KC = kmax + 1;
+    sv->m = tk_record_len(kmax);
+    sv->symmetric = symmetric;
+    sv->bnorm = b_norm;
+    sv->lmin.assign(lmin, lmin + kmax);
+    sv->rank.assign(rank, rank + kmax);
+    sv->roff.assign(kmax, 0);
+    int tot = 0;
+    for (int k = 0; k < kmax; ++k) {
+        if (rank[k] < 0) {
+            delete sv;
+            return tk_fail_internal(TK_ERR_ARG, "tk_solver_create: negative rank");
+        }
+        sv->roff[k] = tot;
+        tot += rank[k];
+    }
+    sv->alpha.assign(alpha, alpha + tot);
+    sv->omega.assign(omega, omega + tot);
+    sv->H.assign((size_t)d * sv->KP * sv->KC, 0.0);
+    sv->bt.assign((size_t)d * sv->KC, 0.0);
+    sv->gram0.assign((size_t)sv->KC * sv->KC, 0.0);
+    sv->loss.assign((size_t)d * sv->KC, 0.0);
+    sv->reorth.assign((size_t)d * sv->KC, 0);
+    *out = sv;
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_overlay(tk_solver* sv, int first, int nf, const double* records) { TK_API_BEGIN
+    if (!sv || first < 0 || nf < 0 || first + nf > sv->d) return tk_fail_internal(TK_ERR_ARG, "tk_solver_overlay: bad argument");
+    if (!records) {
+        sv->overlay.clear();
+        return TK_OK;
+    }
+    sv->overlay.assign(records, records + (size_t)(sv->kmax + 2) * sv->d * sv->m);
+    sv->ov_first = first;
+    sv->ov_nf = nf;
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_destroy(tk_solver* sv) {
+    delete sv;
+    return TK_OK;
+}
+
+tk_status tk_solver_apply(tk_solver* sv, int j, const double* rec) { TK_API_BEGIN
+    if (!sv || !rec || j < -1 || j >= sv->kmax) return tk_fail_internal(TK_ERR_ARG, "tk_solver_apply: bad argument");
+    apply_record(sv, j, rec);
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_evaluate(tk_solver* sv, int k, double* out4) { TK_API_BEGIN
+    if (!sv || !out4 || k < 2 || k > sv->kmax || sv->rank[k - 1] < 1)
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_evaluate: bad argument");
+    evaluate(sv, k, sv->last, sv->ws);
+    out4[0] = sv->last.r_comp;
+    out4[1] = sv->last.r_norm;
+    out4[2] = sv->last.rel;
+    out4[3] = sv->last.orth;
+    if (sv->last.status == TK_ERR_STATE) return tk_fail_internal(TK_ERR_STATE, "compressed solve failed (eigen / expm)");
+    return sv->last.status;
+    TK_API_END
+}
+
+int tk_solver_rank(tk_solver* sv, int k) { return (sv && k >= 1 && k <= sv->kmax) ? sv->rank[k - 1] : -1; }
+
+tk_status tk_solver_solution(tk_solver* sv, int k, double* lambda_out, double* Y_out) { TK_API_BEGIN
+    if (!sv || sv->last.k != k || !lambda_out || !Y_out)
+        return tk_fail_internal(TK_ERR_STATE, "tk_solver_solution: iteration k was not the last evaluated");
+    memcpy(lambda_out, sv->last.lam.data(), sv->last.lam.size() * sizeof(double));
+    memcpy(Y_out, sv->last.Y.data(), sv->last.Y.size() * sizeof(double));
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_state(tk_solver* sv, double* H_out, double* bt_out, double* gram0_out) { TK_API_BEGIN
+    if (!sv) return tk_fail_internal(TK_ERR_ARG, "NULL solver");
+    const int KP = sv->KP, KC = sv->KC;
+    if (H_out)   // [s][r][c] row-major (the host mirror's layout)
+        for (int s = 0; s < sv->d; ++s)
+            for (int r = 0; r < KP; ++r)
+                for (int c = 0; c < KC; ++c)
+                    H_out[((size_t)s * KP + r) * KC + c] = sv->H[(size_t)s * KP * KC + (size_t)c * KP + r];
+    if (bt_out) memcpy(bt_out, sv->bt.data(), sv->bt.size() * sizeof(double));
+    if (gram0_out) memcpy(gram0_out, sv->gram0.data(), sv->gram0.size() * sizeof(double));
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, int depth, int nthreads,
+                        double* relres, double* projres, double* orth, int* k_end, int* outcome) { TK_API_BEGIN
+    if (!sv || !dc || !relres || !projres || !orth || !k_end || !outcome || kfirst < 2)
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_run: bad argument");
+    const int kmax = sv->kmax;
+    int klast = kmax;   // iterations with a tabulated exp-sum rank
+    for (int k = kfirst; k <= kmax; ++k)
+        if (sv->rank[k - 1] < 1) {
+            klast = k - 1;
+            break;
+        }
+    const int P = std::max(1, std::min(nthreads, 64));
+    depth = std::max(depth, P + 1);
+    *outcome = 0;
+    *k_end = klast;
+    std::vector<double> rec((size_t)sv->d * sv->m);
+    // steps kfirst .. kfirst+depth-1 ahead of the first evaluation (step k is ABI step k-1)
+    int next_issue = kfirst;
+    auto issue_upto = [&](int kk) -> tk_status {
+        for (; next_issue <= std::min(kk, kmax); ++next_issue) {
+            tk_status st = tk_decomp_step(dc, next_issue - 1, nullptr);
+            if (st) return st;
+        }
+        return TK_OK;
+    };
+    tk_status st = issue_upto(kfirst + depth - 1);
+    if (st) return st;
+
+    std::vector<Worker> workers(P);
+    Pool pool;
+    pool.done.assign(P, 0);
+    for (int w = 0; w < P; ++w)
+        workers[w].th = std::thread([sv, w, &wk = workers[w], &pool] {
+            for (;;) {
+                int k;
+                {
+                    std::unique_lock<std::mutex> lk(wk.mu);
+                    wk.cv.wait(lk, [&] { return wk.job != 0; });
+                    k = wk.job;
+                }
+                if (k < 0) return;
+                evaluate(sv, k, wk.res, wk.ws);
+                {
+                    std::lock_guard<std::mutex> lk(wk.mu);
+                    wk.job = 0;
+                }
+                {
+                    std::lock_guard<std::mutex> lk(pool.mu);
+                    pool.done[w] = k;
+                }
+                pool.cv.notify_all();
+            }
+        });
+    auto submit = [&](int w, int k) {
+        {
+            std::lock_guard<std::mutex> lk(pool.mu);
+            pool.done[w] = 0;
+        }
+        {
+            std::lock_guard<std::mutex> lk(workers[w].mu);
+            workers[w].job = k;
+        }
+        workers[w].cv.notify_one();
+    };
+    auto wait_done = [&](int w, int k) {
+        std::unique_lock<std::mutex> lk(pool.mu);
+        pool.cv.wait(lk, [&] { return pool.done[w] == k; });
+    };
+    auto stop_workers = [&] {
+        for (auto& wk : workers) {
+            {
+                std::unique_lock<std::mutex> lk(wk.mu);
+                // a job still in flight finishes first (its result is discarded)
+                while (wk.job > 0) {
+                    lk.unlock();
+                    std::this_thread::yield();
+                    lk.lock();
+                }
+                wk.job = -1;
+            }
+            wk.cv.notify_one();
+        }
+        for (auto& wk : workers) wk.th.join();
+    };
+
+    int k_dispatch = kfirst;
+    tk_status err = TK_OK;
+    // TKHIP_SOLVER_STATS=1: where the calling thread's time goes (stderr)
+    const char* est = getenv("TKHIP_SOLVER_STATS");
+    const bool stats = est && est[0] == '1';
+    typedef std::chrono::steady_clock clk;
+    double t_rec = 0, t_issue = 0, t_apply = 0, t_wait = 0;
+    auto tp = clk::now();
+    auto lap = [&](double& acc) {
+        if (!stats) return;
+        const auto now = clk::now();
+        acc += std::chrono::duration<double, std::micro>(now - tp).count();
+        tp = now;
+    };
+    const auto t_begin = clk::now();
+    for (int k = kfirst; k <= klast; ++k) {
+        // keep P evaluations in flight: records of step k_dispatch-1, applied in order
+        while (k_dispatch <= klast && k_dispatch < k + P) {
+            lap(t_wait);
+            err = tk_decomp_records(dc, k_dispatch, k_dispatch + 1, rec.data());
+            lap(t_rec);
+            if (!err) err = issue_upto(k_dispatch + depth);
+            lap(t_issue);
+            if (err) break;
+            apply_record(sv, k_dispatch - 1, rec.data());
+            submit((k_dispatch - kfirst) % P, k_dispatch);
+            ++k_dispatch;
+            lap(t_apply);
+        }
+        if (err) break;
+        Worker& wk = workers[(k - kfirst) % P];
+        wait_done((k - kfirst) % P, k);
+        lap(t_wait);
+        IterResult& r = wk.res;
+        if (r.status == TK_ERR_STATE) {
+            err = tk_fail_internal(TK_ERR_STATE, "compressed solve failed (eigen / expm)");
+            break;
+        }
+        if (r.status == TK_BREAKDOWN) {                       // CompressedNormBreakdown (:85-96)
+            projres[k - 1] = r.r_comp;
+            *outcome = 2;
+            *k_end = k - 1;
+            break;
+        }
+        relres[k - 1] = r.rel;
+        projres[k - 1] = r.r_comp;
+        orth[k - 1] = r.orth;
+        if (r.rel < tol) {                                    // convergence (:108-118)
+            *outcome = 1;
+            *k_end = k;
+            std::swap(sv->last, r);
+            break;
+        }
+        if (k == klast) std::swap(sv->last, r);
+    }
+    stop_workers();
+    if (stats)
+        fprintf(stderr, "tk_solver_run: %d iterations, %d threads, %.1f us total: records %.1f, issue %.1f, "
+                        "apply+submit %.1f, wait results %.1f (us per iteration)\n",
+                *k_end - kfirst + 1, P,
+                std::chrono::duration<double, std::micro>(clk::now() - t_begin).count(),
+                t_rec / std::max(1, *k_end - kfirst + 1), t_issue / std::max(1, *k_end - kfirst + 1),
+                t_apply / std::max(1, *k_end - kfirst + 1), t_wait / std::max(1, *k_end - kfirst + 1));
+    return err;
+    TK_API_END
+}
+
+}  // extern "C"

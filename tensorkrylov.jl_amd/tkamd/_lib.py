@@ -68,6 +68,15 @@ def lib():
         "tk_timing_read": (I, [P, I, DP, ctypes.POINTER(ctypes.c_long)]),
         "tk_compressed_solve": (I, [I, I, DP, I, DP, I, DP, DP, ctypes.c_double, DP, DP]),
         "tk_residualnorm": (I, [I, I, I, DP, DP, DP, DP, DP, ctypes.c_double, DP, DP]),
+        "tk_solver_create": (I, [I, I, I, I, ctypes.c_double, DP, ctypes.POINTER(I), DP, DP, ctypes.POINTER(P)]),
+        "tk_solver_destroy": (I, [P]),
+        "tk_solver_overlay": (I, [P, I, I, DP]),
+        "tk_solver_apply": (I, [P, I, DP]),
+        "tk_solver_evaluate": (I, [P, I, DP]),
+        "tk_solver_rank": (I, [P, I]),
+        "tk_solver_solution": (I, [P, I, DP, DP]),
+        "tk_solver_state": (I, [P, DP, DP, DP]),
+        "tk_solver_run": (I, [P, P, ctypes.c_double, I, I, I, DP, DP, DP, ctypes.POINTER(I), ctypes.POINTER(I)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(L, name)
@@ -85,7 +94,9 @@ EXPORTS = ("tk_last_error", "tk_version", "tk_ctx_create", "tk_ctx_destroy", "tk
            "tk_decomp_exchange_signalled", "tk_decomp_init",
            "tk_decomp_step", "tk_decomp_sweep", "tk_decomp_flush", "tk_decomp_records",
            "tk_decomp_get_basis", "tk_decomp_basis_mul", "tk_timing_enable", "tk_timing_read",
-           "tk_compressed_solve", "tk_residualnorm")
+           "tk_compressed_solve", "tk_residualnorm", "tk_solver_create", "tk_solver_destroy", "tk_solver_overlay",
+           "tk_solver_apply", "tk_solver_evaluate", "tk_solver_rank", "tk_solver_solution", "tk_solver_state",
+           "tk_solver_run")
 
 TK_BREAKDOWN = 7
 

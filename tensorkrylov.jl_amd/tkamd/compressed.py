@@ -218,3 +218,121 @@ def orthogonality_loss_from_gram(G, k):
     Gk = np.tril(G[:k, :k])
     D = Gk + np.tril(Gk, -1).T - np.eye(k)
     return float(np.linalg.norm(D))
+
+
+# ------------------------------------------------------------------ native iteration driver
+
+class IterationTables:
+    """SpectralData / ApproximationData for every iteration k = 2..nmax, computed up front:
+    they depend on A and tol only (src/eigenvalues.jl:353-370, src/approximation.jl:65-175),
+    so the native driver (tk_solver) gets them per k.  If the approximation data run out at
+    some k (kappa beyond the coefficient tables), `error` holds the exception the reference
+    would raise at that iteration and rank[k-1:] = 0."""
+
+    def __init__(self, A, nmax, tol, d=None):
+        d = len(A) if d is None else d
+        spectral = SpectralData(A, nmax)
+        approx = ApproximationData(tol, A.symmetric)
+        self.lmin = np.zeros(nmax)
+        self.rank = np.zeros(nmax, dtype=np.int32)
+        al, om = [], []
+        self.error = None
+        self.error_k = None
+        for k in range(2, nmax + 1):
+            spectral.update(d)
+            try:
+                approx.update(spectral)
+            except ValueError as e:
+                self.error, self.error_k = e, k
+                break
+            self.lmin[k - 1] = spectral.lmin[k - 1]
+            self.rank[k - 1] = len(approx.alpha)
+            al.append(np.asarray(approx.alpha, dtype=np.float64))
+            om.append(np.asarray(approx.omega, dtype=np.float64))
+        self.alpha = np.ascontiguousarray(np.concatenate(al) if al else np.zeros(1))
+        self.omega = np.ascontiguousarray(np.concatenate(om) if om else np.zeros(1))
+
+
+class NativeSolver:
+    """tk_solver: the per-iteration host work of tensorkrylov! in native code (csrc/
+    tk_solver.cpp) -- record bookkeeping, compressed solve, residual, orthogonality of V_1 --
+    and the pipelined loop over a device decomposition with iterations evaluated on a pool
+    of host threads."""
+
+    def __init__(self, method, d, kmax, symmetric, b_norm, tables):
+        import ctypes
+        from . import _lib as L
+        self._L = L
+        self.d, self.kmax = d, kmax
+        self.tables = tables
+        h = ctypes.c_void_p()
+        rank = np.ascontiguousarray(tables.rank, dtype=np.int32)
+        self._rank = rank
+        L.check(L.lib().tk_solver_create(int(method), int(d), int(kmax), 1 if symmetric else 0,
+                                         ctypes.c_double(b_norm), L.dptr(tables.lmin),
+                                         rank.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                         L.dptr(tables.alpha), L.dptr(tables.omega), ctypes.byref(h)))
+        self.h = h
+
+    def overlay(self, first, nf, records):
+        """Emulation only: rows of factors outside [first, first+nf) come from `records`
+        ([kmax+2][d][m], a full run's) whenever records are applied (tk_solver_overlay)."""
+        self._ov = None if records is None else np.ascontiguousarray(records, dtype=np.float64)
+        self._L.check(self._L.lib().tk_solver_overlay(self.h, int(first), int(nf),
+                                                      None if records is None else self._L.dptr(self._ov)))
+
+    def apply(self, j, rec):
+        rec = np.ascontiguousarray(rec, dtype=np.float64)
+        self._L.check(self._L.lib().tk_solver_apply(self.h, int(j), self._L.dptr(rec)))
+
+    def evaluate(self, k):
+        """(r_comp, r_norm, relative residual, orthogonality loss) of iteration k; raises
+        CompressedNormBreakdown like residualnorm!."""
+        out = np.zeros(4)
+        st = self._L.lib().tk_solver_evaluate(self.h, int(k), self._L.dptr(out))
+        if st == self._L.TK_BREAKDOWN:
+            raise CompressedNormBreakdown(out[0])
+        self._L.check(st)
+        return tuple(float(x) for x in out)
+
+    def solution(self, k):
+        t = int(self.tables.rank[k - 1])
+        lam = np.zeros(t)
+        Y = np.zeros((self.d, t, k))
+        self._L.check(self._L.lib().tk_solver_solution(self.h, int(k), self._L.dptr(lam), self._L.dptr(Y)))
+        return lam, [Y[s].T.copy() for s in range(self.d)]
+
+    def state(self):
+        KP, KC = self.kmax + 2, self.kmax + 1
+        H = np.zeros((self.d, KP, KC))
+        bt = np.zeros((self.d, KC))
+        G = np.zeros((KC, KC))
+        self._L.check(self._L.lib().tk_solver_state(self.h, self._L.dptr(H), self._L.dptr(bt),
+                                                    self._L.dptr(G)))
+        return H, bt, G
+
+    def run(self, dev, tol, kfirst=2, depth=2, nthreads=4):
+        """Pipelined loop k = kfirst..kmax on a DeviceDecomposition.  Returns (outcome,
+        k_end, relres, projres, orth) with outcome 0 / 1 / 2 as tk_solver_run."""
+        import ctypes
+        L = self._L
+        rel = np.zeros(self.kmax)
+        proj = np.zeros(self.kmax)
+        orth = np.zeros(self.kmax)
+        k_end = ctypes.c_int()
+        outcome = ctypes.c_int()
+        L.check(L.lib().tk_solver_run(self.h, dev.h, ctypes.c_double(tol), int(kfirst), int(depth),
+                                      int(nthreads), L.dptr(rel), L.dptr(proj), L.dptr(orth),
+                                      ctypes.byref(k_end), ctypes.byref(outcome)))
+        return outcome.value, k_end.value, rel, proj, orth
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.lib().tk_solver_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -98,8 +98,11 @@ class TensorDecomposition:
         """orthonormalize!(td, b) (src/orthogonal_bases.jl:142-160): V[:,1] = b/|b|,
         then step 1 for every factor."""
         self._attach(b)
-        self._apply_gram(self.dev.init())
+        r0 = self.dev.init()
+        self._apply_gram(r0)
+        self.first_records = [(-1, r0)]          # for a native driver taking over (tk_solver)
         self.orthonormalize(1)
+        self.first_records.append((0, self._last_rec))
 
     def orthonormalize(self, k):
         """orthonormalize!(td, k) (src/orthogonal_bases.jl:162-180), k 1-based."""
@@ -124,6 +127,7 @@ class TensorDecomposition:
             rec = self.dev.records(j + 1, j + 2)[0]
         self._apply_step(j, rec)
         self._apply_gram(rec)
+        self._last_rec = rec
 
     def flush(self):
         rec = self.dev.flush()

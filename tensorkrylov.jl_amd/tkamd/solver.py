@@ -11,14 +11,27 @@ import time
 
 import numpy as np
 
-from .compressed import (ApproximationData, CompressedNormBreakdown, SpectralData,
-                         residualnorm, solve_compressed_system)
+from .compressed import (ApproximationData, CompressedNormBreakdown, IterationTables, NativeSolver,
+                         SpectralData, residualnorm, solve_compressed_system)
 from .decompositions import METHODS
 from .structures import ConvergenceData, KruskalTensor, kronprodnorm
 
 
+def _native_threads():
+    import os
+    v = os.environ.get("TKHIP_SOLVER_THREADS")
+    if v:
+        return max(1, int(v))
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    return max(1, min(8, ncpu // 2))
+
+
 def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbose=False,
-                 backend=None, keep_decomposition=False, pipelined=True, depth=2):
+                 backend=None, keep_decomposition=False, pipelined=True, depth=2, native=True,
+                 threads=None, overlay=None):
     """tensorkrylov!(convergence_data, A, b, tol, nmax, orthonormalization_type).
     Returns the approximate solution as a KruskalTensor of the LOCAL factors
     (x_s = V_s y_s) on convergence, else None.
@@ -28,7 +41,15 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
     device never waits for the host's read of a record.  Steps after k leave V[:, 1:k],
     H[1:k, 1:k] and b~[1:k] untouched, so every iterate, residual and the returned solution
     are those of the sequential loop; on convergence at k the extra steps' results are
-    simply never read."""
+    simply never read.
+
+    native: the per-iteration host work (record bookkeeping, compressed solve, residual,
+    orthogonality) runs in libtkhip's tk_solver; on a device decomposition the whole loop
+    does (tk_solver_run: steps enqueued ahead, iterations evaluated on `threads` host
+    threads, consumed in order -- the same iterates).  native=False keeps the Python loop
+    below (the mirror of the reference's driver, used to cross-check the native one).
+    overlay (diagnostic, native only): a full run's records [nmax+2][d][m]; the records of
+    factors this rank does not own are taken from it (bench.py --emulate-ranks)."""
     if isinstance(method, str):
         method = METHODS[method]
     d = len(A)
@@ -40,6 +61,23 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
     conv.timing = {}
     try:
         td.orthonormalize_first(b)                                  # :53 (+ b~ init, :55)
+        if native:
+            # setup: spectral bounds + exp-sum data of every k (functions of A and tol only)
+            # and the native driver holding the records of init and step 1
+            t_tab = time.perf_counter()
+            tables = IterationTables(A, nmax, tol, d)
+            conv.timing["tables_s"] = time.perf_counter() - t_tab
+            sv = NativeSolver(td.method, d, nmax, symmetric, b_norm, tables)
+            try:
+                if overlay is not None:
+                    sv.overlay(td.part.first, td.part.nf, overlay)
+                for j, rec in td.first_records:
+                    sv.apply(j, rec)
+                t_loop = time.perf_counter()
+                conv.timing["setup_s"] = t_loop - t_start
+                return _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, threads, t_loop)
+            finally:
+                sv.close()
         t_loop = time.perf_counter()
         conv.timing["setup_s"] = t_loop - t_start                   # upload A_s, b_s; step 1
         spectral = SpectralData(A, nmax)                            # :57
@@ -95,6 +133,66 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             conv.decomposition = td
         else:
             td.close()
+
+
+def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, threads, t_loop):
+    """tensorkrylov!'s loop (src/tensor_krylov_method.jl:57-125) through tk_solver; loop_s
+    covers the iterations only (the host mirror is copied back afterwards)."""
+    device = hasattr(td.dev, "h") and hasattr(td.dev, "records")
+    if device and pipelined:
+        nthr = threads or _native_threads()
+        outcome, k_end, rel, proj, orth = sv.run(td.dev, tol, 2, max(depth, nthr + 1), nthr)
+        conv.relative_residual_norm[1:k_end] = rel[1:k_end]
+        conv.projected_residual_norm[1:k_end] = proj[1:k_end]
+        conv.orthogonality_data[1:k_end] = orth[1:k_end]
+    else:
+        outcome, k_end = 0, nmax
+        for k in range(2, nmax + 1):
+            if tables.rank[k - 1] < 1:
+                k_end = k - 1
+                break
+            td.orthonormalize(k)                                    # :66
+            sv.apply(k - 1, td._last_rec)
+            try:
+                r_comp, _, rel_k, orth_k = sv.evaluate(k)           # :68-103
+            except CompressedNormBreakdown:
+                outcome, k_end = 2, k - 1
+                break
+            conv.relative_residual_norm[k - 1] = rel_k
+            conv.projected_residual_norm[k - 1] = r_comp
+            conv.orthogonality_data[k - 1] = orth_k
+            if rel_k < tol:
+                outcome, k_end = 1, k
+                break
+    x = None
+    if outcome == 1:                                                # :108-118
+        lam, Ys = sv.solution(k_end)
+        loc = list(td.part.local())
+        X = td.dev.basis_mul(k_end, [Ys[s] for s in loc])
+        x = KruskalTensor(lam.copy(), X)
+        x.factors = loc
+    conv.timing["loop_s"] = time.perf_counter() - t_loop
+    # the host mirror of H, b~ and factor 1's Gram rows (principal_minors readers)
+    H, bt, G = sv.state()
+    td.H[...] = H
+    td.btilde[...] = bt
+    if 0 in td.gram:
+        td.gram[0][...] = G
+    if outcome == 2:                                                # :85-96
+        if verbose:
+            print("Early termination at k = %d due to compressed norm breakdown" % (k_end + 1))
+        conv.niterations = k_end
+        conv.resize(k_end)
+        return None
+    if outcome == 1:
+        if verbose:
+            print("Convergence")
+        return x
+    if k_end < nmax and tables.error is not None:
+        raise tables.error
+    if verbose:
+        print("No convergence")
+    return None
 
 
 def solve_tensorized_system(system, nmax, method, tol=1e-9, **kw):

@@ -225,6 +225,62 @@ def test_driver_host_logic_matches_oracle(method, cls, sym, d, K):
     assert np.allclose(conv.orthogonality_data[1:], conv_o.orthogonality_data[1:], rtol=1e-6, atol=1e-15)
 
 
+@pytest.mark.parametrize("method,cls,sym,d,K,tol", [("TensorArnoldi", "Laplace", True, 4, 40, 1e-9),
+                                                      ("TensorLanczosReorth", "Laplace", True, 3, 30, 1e-9),
+                                                      ("TensorLanczos", "Laplace", True, 3, 25, 1e-9),
+                                                      ("TensorArnoldi", "ConvDiff", False, 3, 15, 1e-9),
+                                                      ("TensorArnoldi", "Laplace", True, 2, 40, 1e-6)])
+def test_native_iteration_driver_matches_python_loop(method, cls, sym, d, K, tol):
+    """tk_solver (native record bookkeeping + compressed solve + residual + orthogonality)
+    against the Python mirror of the reference's loop on the same records: the host mirror
+    of H and b~ bit for bit, the trajectories to rounding, the same stopping iteration and
+    the same solution factors."""
+    from _fake_device import backend
+    n = 200
+    rng = np.random.default_rng(99)
+    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    inst = tkamd.SymInstance if sym else tkamd.NonSymInstance
+    A = tkamd.KroneckerMatrix.gallery(inst, d, n, cls)
+    out = []
+    for native in (False, True):
+        conv = tkamd.ConvergenceData(K)
+        x = tkamd.tensorkrylov(conv, A, [v.copy() for v in b], tol, K, method, backend=backend,
+                               native=native, keep_decomposition=True)
+        out.append((conv, x))
+    (cp, xp), (cn, xn) = out
+    assert cp.niterations == cn.niterations
+    kk = cp.niterations
+    assert np.array_equal(cp.decomposition.H[:, :kk + 1, :kk], cn.decomposition.H[:, :kk + 1, :kk])
+    assert np.array_equal(cp.decomposition.btilde[:, :kk], cn.decomposition.btilde[:, :kk])
+    ref = cp.relative_residual_norm
+    assert np.abs(cn.relative_residual_norm - ref).max() <= 1e-12 * ref.max()
+    assert np.allclose(cn.projected_residual_norm, cp.projected_residual_norm, rtol=1e-9, atol=1e-12)
+    assert np.allclose(cn.orthogonality_data, cp.orthogonality_data, rtol=1e-9, atol=1e-15)
+    assert (xp is None) == (xn is None)
+    if xp is not None:
+        assert np.allclose(xn.lam, xp.lam, rtol=1e-15)
+        for a_, b_ in zip(xn.fmat, xp.fmat):
+            assert np.abs(a_ - b_).max() <= 1e-12 * max(1.0, np.abs(b_).max())
+
+
+def test_native_iteration_tables_match_python_updates():
+    """IterationTables (spectral bounds and exp-sum data per k, computed up front) equal the
+    per-iteration updates of the Python loop."""
+    d, n, K = 3, 300, 30
+    A = tkamd.KroneckerMatrix.gallery(tkamd.SymInstance, d, n, tkamd.Laplace)
+    T = tkamd.compressed.IterationTables(A, K, 1e-9, d)
+    spec = tkamd.SpectralData(A, K)
+    apx = tkamd.ApproximationData(1e-9, True)
+    off = 0
+    for k in range(2, K + 1):
+        spec.update(d)
+        apx.update(spec)
+        t = len(apx.alpha)
+        assert T.rank[k - 1] == t and T.lmin[k - 1] == spec.lmin[k - 1]
+        assert np.array_equal(T.alpha[off:off + t], apx.alpha) and np.array_equal(T.omega[off:off + t], apx.omega)
+        off += t
+
+
 # ------------------------------------------------------------------ single-matrix drivers (a12)
 def test_single_matrix_drivers_host_logic():
     """arnoldi_algorithm / lanczos_algorithm / isorthonormal (src/orthogonal_bases.jl:182-284)
