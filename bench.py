@@ -10,7 +10,9 @@ One bench "step" = one full device sweep of the iteration: V[:,1] = b/|b|, then 
 K = 50 orthonormalize!(td, k) iterations over all d factors (k = 1..50; each one the
 SpMV + MGS2 step of every factor plus update_rhs!'s <V_k, b_s> and factor 1's Gram
 row), with the per-iteration RCCL all-reduce of the factors' records when N > 1, and
-the final basis_tensor_mul! X_s = V_s Y_s (t = the exp-sum rank at k = 50) on MFMA.
+the final basis_tensor_mul! X_s = V_s Y_s (t = the exp-sum rank at k = 50), which also
+finalizes the last basis column (fused into one pass over V for Arnoldi; the MFMA
+V*Y kernel is timed beside it as basis_mul_mfma).
 Inputs are resident in HBM before timing.  value = K * steps / time (whole job).
 Factors are partitioned over ranks (one process per GPU): the total work is fixed, so
 the scaling is STRONG (see DESIGN.md "Multi-GPU").
@@ -153,8 +155,7 @@ def main():
         dev.sweep(0, K)                 # enqueues K steps; returns before they run
         host_issue[0] += time.perf_counter() - h0
         host_issue[1] += 1
-        dev.flush(False)
-        dev.basis_mul(K, Ys, want=False)
+        dev.basis_mul(K, Ys, want=False)   # finalizes the pending column V[:, K] first (fused for Arnoldi)
 
     def barrier():
         ctx.sync()
@@ -198,6 +199,14 @@ def main():
                          ("reduce_post", L.T_RED), ("basis_mul", L.T_VY), ("exchange", L.T_XCH)):
         ms, cnt = ctx.timing_read(cls_id)
         kern[name] = {"avg_us": round(1e3 * ms / cnt, 3) if cnt else None, "launches": cnt}
+    ctx.timing(0)
+    # the standalone V*Y on MFMA (v_mfma_f64_16x16x4f64; what basis_mul runs when no column
+    # is pending, or without the fused flush), on the same basis: untimed above
+    ctx.timing(1)
+    for _ in range(3):
+        dev.basis_mul(K, Ys, want=False)
+    ctx.sync()
+    mf_ms, mf_cnt = ctx.timing_read(L.T_VY)
     ctx.timing(0)
 
     # end-to-end: the whole tensorkrylov! loop (device steps + the host's compressed solve,
@@ -264,6 +273,8 @@ def main():
     vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
     vy_flops = 2 * n * K * t_rank * part.nf
     vy_s = (vy_ms / 1e3) / max(vy_cnt, 1)
+    mf_s = (mf_ms / 1e3) / max(mf_cnt, 1)
+    fused_vy = method == "TensorArnoldi"      # the step's basis_mul finalizes the pending column with it
 
     out = None
     if rank == 0:
@@ -322,10 +333,15 @@ def main():
             },
             "host_issue_us_per_iteration": round(host_us_per_step, 2),
             "end_to_end": e2e,
-            "basis_mul_mfma": {
+            "basis_mul_step": {
+                "engine": ("k_fin_vy: flush of the pending column + V*Y from its register row (FP64 FMA), "
+                           "one read of V" if fused_vy else "k_basis_mul (MFMA) after the flush"),
                 "avg_us": round(vy_s * 1e6, 2),
-                "GB_s": round(vy_bytes / vy_s / 1e9, 1) if vy_cnt else None,
-                "TFLOP_s": round(vy_flops / vy_s / 1e12, 3) if vy_cnt else None,
+            },
+            "basis_mul_mfma": {
+                "avg_us": round(mf_s * 1e6, 2),
+                "GB_s": round(vy_bytes / mf_s / 1e9, 1) if mf_cnt else None,
+                "TFLOP_s": round(vy_flops / mf_s / 1e12, 3) if mf_cnt else None,
                 "mfma_fp64_peak_TF": FP64_MFMA_PEAK_TF,
             },
             "kernels": kern,

@@ -180,7 +180,11 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
  * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).
  * Y: host [nf][t][k] (each Y_s column-major k x t).  X: host [nf][t][n] (column-major
  * n x t each) or NULL to leave the product on the device (benchmarks).
- * Flushes a pending column first. */
+ * A pending column is finalized first (as tk_decomp_flush, its record in the flush slot);
+ * for TK_ARNOLDI with k <= the step count <= 64, in the same launch as the product: the
+ * flush's register row of each basis tile also forms the product (FP64 FMAs, Y through the
+ * scalar cache), so V is streamed once for both; otherwise (and with TKHIP_NO_FUSED_FLUSH=1)
+ * the flush runs first and the product on v_mfma_f64_16x16x4f64. */
 tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, double* X);
 
 /* ---------------------------------------------------------------- timing hooks */

@@ -1234,11 +1234,19 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
     CHECKARG(k >= 1 && k <= dc->kmax + 1 && t >= 1, "bad k/t");
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
-    if (dc->pending && k - 1 > dc->last_j) {
+    if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
+    // a pending column is finalized first; for Arnoldi with the one-tile flush kernel it is
+    // done in the same launch as V*Y (each basis tile streamed once for both)
+    const int jl = dc->last_j;
+    const char* nofuse = getenv("TKHIP_NO_FUSED_FLUSH");
+    const bool fuse = dc->pending && dc->method == TK_ARNOLDI && dc->fin_d && jl + 1 <= D1_JMAX &&
+                      k <= jl + 1 && !(nofuse && nofuse[0] == '1');
+    const int ldy = fuse ? 64 : k;   // fused: Y_s columns zero-padded to the register row's width
+    if (dc->pending && !fuse) {
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;
     }
-    const size_t ny = (size_t)dc->nf * k * t, nx = (size_t)dc->nf * dc->ld * t;
+    const size_t ny = (size_t)dc->nf * ldy * t, nx = (size_t)dc->nf * dc->ld * t;
     if (ny > dc->ycap) {
         if (dc->Ydev) hipFree(dc->Ydev);
         dc->Ydev = nullptr;
@@ -1252,9 +1260,34 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
         dc->xcap = nx;
     }
     hipStream_t s = c->stream;
-    HIPCHK(hipMemcpyAsync(dc->Ydev, Y, ny * sizeof(double), hipMemcpyHostToDevice, s));
-    KArgs a = base_args(dc, 0, 0);
-    RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");
+    if (fuse) {
+        // Y_s columns zero-padded to ldy rows (tiny: nf * t * 64 doubles); a pageable-source
+        // copy is staged before hipMemcpyAsync returns, as for the caller's Y below
+        std::vector<double> yp(ny, 0.0);
+        for (int f = 0; f < dc->nf; ++f)
+            for (int q = 0; q < t; ++q)
+                memcpy(&yp[((size_t)f * t + q) * ldy], Y + ((size_t)f * t + q) * k, (size_t)k * sizeof(double));
+        HIPCHK(hipMemcpyAsync(dc->Ydev, yp.data(), ny * sizeof(double), hipMemcpyHostToDevice, s));
+    } else {
+        HIPCHK(hipMemcpyAsync(dc->Ydev, Y, ny * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    if (fuse) {
+        const int slot = dc->kmax + 1;
+        tk_status st = slot_guard(dc, slot);
+        if (st) return st;
+        KArgs a = base_args(dc, jl, slot);
+        KArgs f = a;
+        if (dc->onesweep && jl <= D1_JMAX) f.ubuf = (jl & 1) ? 0 : 1;   // as finalize_pending
+        RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, s), "fin_vy");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 1, jl + 3, dc->ntiles, s), "reduce");
+        RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");
+        dc->pending = false;
+        st = exchange_and_copy(dc, slot, nullptr);
+        if (st) return st;
+    } else {
+        KArgs a = base_args(dc, 0, 0);
+        RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");
+    }
     if (X) {
         HIPCHK(hipStreamSynchronize(s));
         for (int f = 0; f < dc->nf; ++f)

@@ -972,14 +972,11 @@ __global__ __launch_bounds__(TPB) void k_init_bd(const DFac* __restrict__ F, KAr
 //   P1 = [ <v,b> | gram <V[:,c],v> (c<=j) | <v,v> ]  (gram and <v,v>: tracked)  (POST_LAN_FIN)
 // For j + 1 <= 64 columns (the register row); beyond, and for gated launches, the
 // tile-loop kernels above.
-template <int MAXC, int MODE>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
-void k_fin_d(const DFac* __restrict__ F, KArgs a) {
+template <int MAXC, int MODE, bool VY = false>
+__device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int slot, double* lds,
+                                           const double* __restrict__ Yf = nullptr, double* __restrict__ Xf = nullptr,
+                                           int ldy = 0, int tq = 0) {
     constexpr int NG = (MAXC + 15) / 16;
-    extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
-    const DFac& d = F[blockIdx.y];
-    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
-    if (slot >= a.ntiles) return;
     const int j = a.j, nc = j + 1, t = threadIdx.x;
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     const int64_t r = (int64_t)slot * TPB + t;
@@ -1018,6 +1015,19 @@ void k_fin_d(const DFac* __restrict__ F, KArgs a) {
         v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
     }
     st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, ((j + 1) & 1) ? R.last : 0.0);
+    if constexpr (VY) {
+        // X_s[r, q] = sum_{c < k} V[r, c] Y_s[c, q] from the register row the flush just
+        // loaded (the tile is streamed once for both); Y_s columns zero-padded to ldy >= MAXC
+        // (so columns k..j of the row meet zeros), read through the scalar cache two at a time
+        for (int q = 0; q < tq; q += 2) {
+            double x0, x1;
+            row_dot2<MAXC>(R, Yf + (int64_t)q * ldy, Yf + (int64_t)(q + 1 < tq ? q + 1 : q) * ldy, x0, x1);
+            if (ok) {
+                st(Xf, r + (int64_t)q * a.ld, x0);
+                if (q + 1 < tq) st(Xf, r + (int64_t)(q + 1) * a.ld, x1);
+            }
+        }
+    }
     if (gram) {
 #pragma unroll
         for (int k = 0; k < NG; ++k) {
@@ -1051,6 +1061,16 @@ void k_fin_d(const DFac* __restrict__ F, KArgs a) {
         }
         if (vi >= 0) st(d.P1, (int64_t)vi * a.ntiles + slot, sum);
     }
+}
+
+template <int MAXC, int MODE>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
+void k_fin_d(const DFac* __restrict__ F, KArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
+    const DFac& d = F[blockIdx.y];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= a.ntiles) return;
+    fin_d_tile<MAXC, MODE>(d, a, slot, lds);
 }
 
 // ------------------------------------------------------------------ Lanczos (TTR)
@@ -1653,21 +1673,20 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // Each D register store covers 4 consecutive rows of 16 columns; the four registers
 // of a strip complete 16-row runs that the L2 merges before write-back.
 #define YS_STRIDE 72   // LDS row stride of Ys: rows 2*slot apart land 32 banks apart
+#define XS_STRIDE 260  // LDS column stride of the staged X tile: a 64-lane b64 write is 2-way (optimal)
+#define BM_LDS_DOUBLES (64 * YS_STRIDE)   // Ys; the X staging (16 x XS_STRIDE) reuses it
+// One 256-row tile of X_s[:, t0 .. t0+16NG) = V_s[:, 0..k) Y_s on v_mfma_f64_16x16x4f64: wave w
+// owns rows 64w .. 64w+63 (four 16-row groups), 16-column groups q < NG; Y staged in LDS per
+// 64-deep k chunk.  The accumulators go through LDS (16 columns at a time) so each X column
+// is written as 256 contiguous rows (full lines) instead of 32-B pieces.
 template <int NG>
-__global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
-                                                   const double* __restrict__ Yall,
-                                                   double* __restrict__ Xall, int k, int t) {
-    __shared__ double Ys[64 * YS_STRIDE];   // [kk][col] of one 64-deep k chunk
-    const int f = blockIdx.y;
-    const DFac& d = F[f];
+__device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, const double* __restrict__ Y,
+                                               double* __restrict__ X, int k, int t, int tile, int t0,
+                                               double* Ys) {
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
-    const double* Y = Yall + (int64_t)f * k * t;
-    double* X = Xall + (int64_t)f * a.ld * t;
-    const int tile = blockIdx.x;
     const double* Vt = d.V + (int64_t)tile * TS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
-    const int t0 = blockIdx.z * 16 * NG;
     const int tn = min(16 * NG, t - t0);
     f64x4 acc[4][NG];
 #pragma unroll
@@ -1706,20 +1725,49 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
             }
         }
     }
+    // epilogue: 16 columns at a time through LDS (Xs[c][row], reusing Ys), then every thread
+    // writes its row of each column -- a wave covers 512 contiguous bytes per column
+    double* Xs = Ys;
+    const int64_t r = (int64_t)tile * TPB + threadIdx.x;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int q = 0; q < NG; ++q) {
+        if (16 * q >= tn) break;
+        __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t rr = (int64_t)tile * TPB + wave * 64 + s * 16 + lk + 4 * i;
-            if (rr < a.n) {
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-                for (int q = 0; q < NG; ++q) {
-                    const int c = q * 16 + lr;
-                    if (c < tn) st(X, rr + (int64_t)(t0 + c) * a.ld, acc[s][q][i]);
-                }
-            }
+            for (int i = 0; i < 4; ++i) Xs[lr * XS_STRIDE + wave * 64 + s * 16 + lk + 4 * i] = acc[s][q][i];
+        __syncthreads();
+        if (r < a.n) {
+            const int cn = min(16, tn - 16 * q);
+            for (int c = 0; c < cn; ++c) st(X, r + (int64_t)(t0 + 16 * q + c) * a.ld, Xs[c * XS_STRIDE + threadIdx.x]);
         }
     }
+}
+
+template <int NG>
+__global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
+                                                   const double* __restrict__ Yall,
+                                                   double* __restrict__ Xall, int k, int t) {
+    __shared__ __attribute__((aligned(16))) double Ys[BM_LDS_DOUBLES];
+    const int f = blockIdx.y;
+    basis_mul_tile<NG>(F[f], a, Yall + (int64_t)f * k * t, Xall + (int64_t)f * a.ld * t, k, t, blockIdx.x,
+                       blockIdx.z * 16 * NG, Ys);
+}
+
+// The pending column's flush (fin_d_tile, MODE 0: Arnoldi) and V * Y of the same tile in one
+// block: the register row the flush loads also feeds the product, so each basis tile is
+// streamed from HBM once for both.  Y: [nf][t][ldy] with zero rows k..ldy-1, k <= j + 1.
+template <int MAXC>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
+void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Yall, double* __restrict__ Xall,
+              int ldy, int t) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
+    const int f = blockIdx.y;
+    const DFac& d = F[f];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= a.ntiles) return;
+    fin_d_tile<MAXC, 0, true>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
 }
 
 // ------------------------------------------------------------------ plain SpMV (test hook)
@@ -1866,6 +1914,15 @@ void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s
     with_maxc(nc, [&](auto Mc) {
         if (mode == 0) hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 0>), grid, dim3(TPB), lds, s, F, a);
         else hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 1>), grid, dim3(TPB), lds, s, F, a);
+    });
+}
+void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s) {
+    const int nc = a.j + 1;
+    const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
+    const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
+    const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
+    with_maxc(nc, [&](auto Mc) {
+        hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
     });
 }
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {

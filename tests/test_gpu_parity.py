@@ -382,3 +382,42 @@ def test_arnoldi_untracked_factors_identical(ctx, orth, monkeypatch):
     for x, y in zip(Va, Vb):
         assert np.array_equal(x, y)
 
+
+
+@pytest.mark.parametrize("cls,n,t", [("Laplace", 3000, 17), ("ConvDiff", 5000, 3), ("Laplace", 1000, 30)])
+def test_fused_flush_basis_mul_identical(ctx, cls, n, t, monkeypatch):
+    """basis_mul on a pending column finalizes it in the same launch as V*Y (k_fin_vy: the
+    product from the flush's register row, FP64 FMAs); the flushed column, its record (Gram
+    row, b-tilde) and the columns before it are bitwise those of the separate flush +
+    basis_mul (TKHIP_NO_FUSED_FLUSH=1, product on MFMA); both products agree with the host
+    product to 1e-13 relative (summation order differs)."""
+    tk = _tk()
+    K = 40
+    csc = tk.assemble_matrix(n, cls)
+    bs = _rhs(n, 3, 31, distinct=True)
+    rng = np.random.default_rng(2)
+    Ys = [rng.standard_normal((K, t)) for _ in range(3)]
+    out = []
+    for fused in (True, False):
+        if fused:
+            monkeypatch.delenv("TKHIP_NO_FUSED_FLUSH", raising=False)
+        else:
+            monkeypatch.setenv("TKHIP_NO_FUSED_FLUSH", "1")
+        A = tk.DeviceMatrix(ctx, csc)
+        dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, 3, 0, [A] * 3, bs, K, track_all_gram=True)
+        dev.init(False)
+        dev.sweep(0, K)
+        X = dev.basis_mul(K, Ys)
+        rec = dev.records(K + 1, K + 2)[0]
+        V = [dev.basis(f, 0, K + 1) for f in range(3)]
+        dev.close()
+        A.close()
+        out.append((X, rec, V))
+    (Xa, ra, Va), (Xb, rb, Vb) = out
+    assert np.array_equal(ra, rb)
+    for a_, b_ in zip(Va, Vb):
+        assert np.array_equal(a_, b_)
+    for f in range(3):                                   # both products against the host product
+        ref = Va[f][:, :K] @ Ys[f]
+        for X in (Xa, Xb):
+            assert np.abs(X[f] - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
