@@ -164,6 +164,7 @@ def main():
 
     if args.pmc_mode:
         sweep()
+        dev.basis_mul(K, Ys, want=False)   # the standalone MFMA V*Y (no column pending now)
         barrier()
         dev.close()
         A.close()
