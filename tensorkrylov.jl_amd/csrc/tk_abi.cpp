@@ -560,6 +560,7 @@ struct tk_decomp {
     bool in_sweep = false;  // inside tk_decomp_sweep: one timing pair for the whole sweep
     bool failed = false;    // a step returned an error: later steps are refused
     int fail_step = -1;     // TKHIP_TEST_FAIL_STEP=j at create: step j reports an error (tests)
+    int skip_mask = 0;      // TKHIP_TEST_SKIP (timing experiments only, wrong results): 1 reduce, 2 post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
@@ -574,6 +575,12 @@ struct tk_decomp {
     // = its sequence number (host-mapped); xslot_seq[slot] = the number to wait for
     unsigned long long* xdone = nullptr;
     std::vector<unsigned long long> xslot_seq;
+    // signalled exchanges are batched: the slots of xgroup consecutive steps go through ONE
+    // all-reduce (TKHIP_XCH_GROUP, default 4); [xp0, xp1] = slots signalled but not yet
+    // exchanged, xev[slot] = the slot whose ev_x marks the exchange that carried it
+    int xgroup = 4;
+    int xp0 = -1, xp1 = -1;
+    std::vector<int> xev;
     hipStream_t cstream = nullptr;          // record copies (multi-rank): no wait on the compute queue
     int last_j = -1;
     std::vector<tk_mat*> mats;
@@ -728,6 +735,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
     if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
+    if (const char* ek = getenv("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
     if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1')))
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
@@ -803,6 +811,9 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
         dc->xslot_seq.assign(kmax + 2, 0);
+        dc->xev.resize(kmax + 2);
+        for (int i = 0; i < kmax + 2; ++i) dc->xev[i] = i;
+        if (const char* eg = getenv("TKHIP_XCH_GROUP")) dc->xgroup = std::min(64, std::max(1, atoi(eg)));
         (void)hipGetLastError();
     }
     c->refs++;
@@ -819,11 +830,14 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
     return dc->onesweep ? 1 : 2;
 }
 
+static tk_status exchange_pending(tk_decomp* dc);
+
 tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     if (!dc) return TK_OK;
     tk_ctx* c = dc->ctx;
     std::vector<tk_mat*> mats = dc->mats;
     hipSetDevice(c->device);
+    if (!dc->failed) exchange_pending(dc);   // (records of slots nobody will read: harmless)
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->xstream);
     free_decomp(dc);
@@ -837,8 +851,8 @@ tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
     // (an already completed exchange needs no wait packet in the compute queue)
-    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[slot]) != hipSuccess)
-        HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[slot], 0));
+    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess)
+        HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
     return TK_OK;
 }
 
@@ -862,34 +876,68 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     return a;
 }
 
-// One RCCL all-reduce per record slot: the send buffer holds only this rank's rows
-// (other rows stay zero forever), so the sum is exact and every rank receives every
-// factor's record.
+// One RCCL all-reduce per group of record slots: the send buffer holds only this rank's
+// rows (other rows stay zero forever), so the sum is exact and every rank receives every
+// factor's record.  Slots [s0, s1] are contiguous in memory, so a group is one call.
+static tk_status exchange_range(tk_decomp* dc, int s0, int s1, bool signalled) {
+    tk_ctx* c = dc->ctx;
+    const size_t cnt = (size_t)dc->d_total * dc->m;
+    double* s = dc->rec + (size_t)s0 * cnt;
+    double* r = dc->recv + (size_t)s0 * cnt;
+    const size_t tot = cnt * (size_t)(s1 - s0 + 1);
+    // the exchange runs on its own stream, overlapping the next steps' kernels; it starts
+    // when the steps' k_post blocks have signalled (or after an event marker)
+    if (signalled) {
+        HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcount, hipStreamWaitValueGte,
+                                    0xFFFFFFFFFFFFFFFFull));
+    } else {
+        HIPCHK(hipEventRecord(dc->ev_c[s1], c->stream));
+        HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[s1], 0));
+    }
+    {
+        Timer tm(c, TCLS_XCH, 2, c->xstream);
+        NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
+    }
+    HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));
+    for (int sl = s0; sl <= s1; ++sl) dc->xev[sl] = s1;
+    if (dc->xdone) {
+        ++dc->seq;
+        for (int sl = s0; sl <= s1; ++sl) dc->xslot_seq[sl] = dc->seq;
+        launch_mirror_records(r, dc->hrec + (size_t)s0 * cnt, (int)tot, dc->xdone + s0, s1 - s0 + 1, dc->seq,
+                              c->xstream);
+        LAUNCHCHK("mirror_records");
+    }
+    return TK_OK;
+}
+
+// Enqueue the exchange of the signalled slots still waiting for their group to fill.
+static tk_status exchange_pending(tk_decomp* dc) {
+    if (dc->xp0 < 0) return TK_OK;
+    const int s0 = dc->xp0, s1 = dc->xp1;
+    dc->xp0 = dc->xp1 = -1;
+    return exchange_range(dc, s0, s1, true);
+}
+
 static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out, bool signalled = false) {
     tk_ctx* c = dc->ctx;
     const size_t cnt = (size_t)dc->d_total * dc->m;
-    double* s = dc->rec + (size_t)slot * cnt;
     double* r = dc->recv + (size_t)slot * cnt;
     if (dc->recv != dc->rec) {
-        // the exchange runs on its own stream, overlapping the next step's kernels; it
-        // starts when the step's k_post blocks have signalled (or after an event marker)
-        if (signalled) {
-            HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcount, hipStreamWaitValueGte,
-                                        0xFFFFFFFFFFFFFFFFull));
-        } else {
-            HIPCHK(hipEventRecord(dc->ev_c[slot], c->stream));
-            HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[slot], 0));
+        if (signalled && !rec_out && dc->xgroup > 1) {
+            // batched: the slot joins the pending group; a full group goes out as one call
+            if (dc->xp0 >= 0 && slot != dc->xp1 + 1) {
+                tk_status st = exchange_pending(dc);
+                if (st) return st;
+            }
+            if (dc->xp0 < 0) dc->xp0 = slot;
+            dc->xp1 = slot;
+            return dc->xp1 - dc->xp0 + 1 >= dc->xgroup ? exchange_pending(dc) : TK_OK;
         }
-        {
-            Timer tm(c, TCLS_XCH, 2, c->xstream);
-            NCCLCHK(ncclAllReduce(s, r, cnt, ncclDouble, ncclSum, c->comm, c->xstream));
-        }
-        HIPCHK(hipEventRecord(dc->ev_x[slot], c->xstream));
-        if (dc->xdone) {
-            dc->xslot_seq[slot] = ++dc->seq;
-            launch_mirror_records(r, dc->hrec + (size_t)slot * cnt, (int)cnt, dc->xdone + slot, dc->seq, c->xstream);
-            LAUNCHCHK("mirror_records");
-        }
+        // exchanges run in slot order: what is pending goes first
+        tk_status st = exchange_pending(dc);
+        if (st) return st;
+        st = exchange_range(dc, slot, slot, signalled);
+        if (st) return st;
         if (rec_out) {
             HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->xstream));
             HIPCHK(hipStreamSynchronize(c->xstream));
@@ -1005,8 +1053,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // flush already wrote it (same operands, same order: the same value).
         a.ubuf = j & 1;
         RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, dc->npd, s), "arn_d1");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN_D, 0, 1, s), "post");
+        if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s), "reduce");
+        if (!(dc->skip_mask & 2)) RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN_D, 0, 1, s), "post");
         dc->pending = true;
     } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
@@ -1105,6 +1153,7 @@ tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) { TK_API_BEGIN
     tk_status st = TK_OK;
     for (int j = j0; j < j1 && st == TK_OK; ++j) st = tk_decomp_step(dc, j, nullptr);
     dc->in_sweep = false;
+    if (st == TK_OK) st = exchange_pending(dc);
     return st;
     TK_API_END
 }
@@ -1138,6 +1187,10 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     HIPCHK(hipSetDevice(dc->ctx->device));
     const size_t per = (size_t)dc->d_total * dc->m;
     if (s1 == s0) return TK_OK;
+    if (dc->xp0 >= 0 && s1 - 1 >= dc->xp0) {
+        tk_status st = exchange_pending(dc);
+        if (st) return st;
+    }
     bool hosted = dc->hdone != nullptr;
     for (int sl = s0; sl < s1 && hosted; ++sl) hosted = dc->slot_seq[sl] != 0;
     if (hosted) {
@@ -1186,7 +1239,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     if (dc->cstream && dc->recv != dc->rec) {
         // multi-rank: the slots are final once the exchange of the last one has run
         // (exchanges run in slot order on the exchange stream); copy on a stream of its own
-        HIPCHK(hipEventSynchronize(dc->ev_x[s1 - 1]));
+        HIPCHK(hipEventSynchronize(dc->ev_x[dc->xev[s1 - 1]]));
         HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                               dc->cstream));
         HIPCHK(hipStreamSynchronize(dc->cstream));

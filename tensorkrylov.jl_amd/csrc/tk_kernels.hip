@@ -1936,21 +1936,21 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
-// Multi-rank host mirror of one all-reduced record slot (runs on the exchange stream after
-// the all-reduce): copy the slot to host-mapped coherent memory, then publish its sequence
-// number, so the host reads the records without any queue call.
+// Multi-rank host mirror of one all-reduced group of record slots (runs on the exchange
+// stream after the all-reduce): copy the slots to host-mapped coherent memory, then publish
+// their sequence number, so the host reads the records without any queue call.
 __global__ __launch_bounds__(TPB) void k_mirror_records(const double* __restrict__ src, double* dst, int cnt,
-                                                        unsigned long long* done, unsigned long long seq) {
+                                                        unsigned long long* done, int nslots, unsigned long long seq) {
     for (int i = threadIdx.x; i < cnt; i += TPB) dst[i] = ld(src, i);
     __syncthreads();
     if (threadIdx.x == 0) {
         __threadfence_system();
-        __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int q = 0; q < nslots; ++q) __hip_atomic_store(done + q, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
-void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, unsigned long long seq,
-                           hipStream_t s) {
-    hipLaunchKernelGGL(k_mirror_records, dim3(1), dim3(TPB), 0, s, src, dst, cnt, done, seq);
+void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
+                           unsigned long long seq, hipStream_t s) {
+    hipLaunchKernelGGL(k_mirror_records, dim3(1), dim3(TPB), 0, s, src, dst, cnt, done, nslots, seq);
 }
 
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {

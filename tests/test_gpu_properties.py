@@ -277,15 +277,41 @@ def test_rccl_exchange_path_matches_local_records(ctx, method, monkeypatch):
     c2.init_comm(tk.unique_id(), 1, 0)
     monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
     # Arnoldi / Lanczos steps trigger the exchange through the signal word (the
-    # hipStreamWaitValue64 path), LanczosReorth through events
-    xch = run(c2, sig=method != 2)
+    # hipStreamWaitValue64 path), LanczosReorth through events; the signalled slots of a
+    # sweep go out in groups (TKHIP_XCH_GROUP; 3 leaves a partial group at the sweep's end)
+    for grp in ("1", "3", "4"):
+        monkeypatch.setenv("TKHIP_XCH_GROUP", grp)
+        xch = run(c2, sig=method != 2)
+        for a, b in zip(local[0], xch[0]):
+            assert np.array_equal(a, b)
+        for s in range(K + 2):
+            assert np.array_equal(local[1][s], xch[1][s])
+        for a, b in zip(local[2], xch[2]):
+            assert np.array_equal(a, b)
     c2.close()
-    for a, b in zip(local[0], xch[0]):
-        assert np.array_equal(a, b)
-    for s in range(K + 2):
-        assert np.array_equal(local[1][s], xch[1][s])
-    for a, b in zip(local[2], xch[2]):
-        assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("grp", ["1", "4", "5"])
+def test_native_loop_through_grouped_exchange(ctx, grp, monkeypatch):
+    """The whole tensorkrylov! loop (native host loop reading records while steps run ahead)
+    over the multi-rank record path with grouped all-reduces: bitwise the local run."""
+    tk = _tk()
+    d, n, K = 4, 3000, 30
+    rng = np.random.default_rng(33)
+    b = [_unit(rng.random(n)) for _ in range(d)]
+    A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
+    ref = tk.ConvergenceData(K)
+    tk.tensorkrylov(ref, A, [v.copy() for v in b], 1e-9, K, "TensorArnoldi", ctx=ctx)
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_XCH_GROUP", grp)
+    conv = tk.ConvergenceData(K)
+    tk.tensorkrylov(conv, A, [v.copy() for v in b], 1e-9, K, "TensorArnoldi", ctx=c2)
+    c2.close()
+    assert conv.niterations == ref.niterations
+    assert np.array_equal(conv.relative_residual_norm, ref.relative_residual_norm)
+    assert np.array_equal(conv.orthogonality_data, ref.orthogonality_data)
 
 
 @pytest.mark.parametrize("method", ["TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"])
