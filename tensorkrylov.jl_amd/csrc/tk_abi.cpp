@@ -561,6 +561,12 @@ struct tk_decomp {
     bool failed = false;    // a step returned an error: later steps are refused
     int fail_step = -1;     // TKHIP_TEST_FAIL_STEP=j at create: step j reports an error (tests)
     int skip_mask = 0;      // TKHIP_TEST_SKIP (timing experiments only, wrong results): 1 reduce, 2 post
+    // one-sweep Arnoldi: the bookkeeping of step bk_j (its record, H column, signals) has not
+    // been enqueued yet; the next step's k_arn_d1 runs it in a spare block (bk_args = the
+    // step's KArgs), or bk_flush launches it on its own
+    int bk_j = -1;
+    KArgs bk_args;
+    bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
@@ -715,13 +721,14 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.U, (size_t)dc->ld * sizeof(double));
         DA(d.P1, (size_t)dc->nvmax * npp * sizeof(double));
         DA(d.P2, (size_t)dc->nvmax * npp * sizeof(double));
-        DA(d.RED1, (size_t)dc->nvmax * sizeof(double));
+        DA(d.RED1, (size_t)std::max(dc->nvmax, RED1_LEN(kmax)) * sizeof(double));
         DA(d.RED2, (size_t)dc->nvmax * sizeof(double));
         DA(d.sc, SC_COUNT * sizeof(double));
         DA(d.h2, (KP + 16) * sizeof(double));   // + COEF_TAIL (tk_kernels.hip)
         DA(d.g, (KP + 16) * sizeof(double));
         DA(d.H, (size_t)KP * KC * sizeof(double));
         DA(d.lossrow, (size_t)KP * sizeof(double));
+        DA(d.ctr, 16);
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
@@ -736,6 +743,8 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
     if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
     if (const char* ek = getenv("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
+    if (const char* eb = getenv("TKHIP_BK_FOLD")) dc->bk_fold = eb[0] != '0';
+    dc->bk_fold = dc->bk_fold && TK_D1_ONEWIN;   // (the window-loop kernel has no bookkeeping blocks)
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
     if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1')))
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
@@ -831,13 +840,17 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
 }
 
 static tk_status exchange_pending(tk_decomp* dc);
+static tk_status bk_flush(tk_decomp* dc, double* rec_out = nullptr);
 
 tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     if (!dc) return TK_OK;
     tk_ctx* c = dc->ctx;
     std::vector<tk_mat*> mats = dc->mats;
     hipSetDevice(c->device);
-    if (!dc->failed) exchange_pending(dc);   // (records of slots nobody will read: harmless)
+    if (!dc->failed) {   // (records of slots nobody will read: harmless)
+        bk_flush(dc);
+        exchange_pending(dc);
+    }
     hipStreamSynchronize(c->stream);
     hipStreamSynchronize(c->xstream);
     free_decomp(dc);
@@ -964,12 +977,37 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
     } while (0);                           \
     LAUNCHCHK(name)
 
+// Step j's record is enqueued (its k_post, or the bookkeeping block of the next k_arn_d1):
+// count its signal, note its host sequence number, and exchange its slot.
+static tk_status complete_step(tk_decomp* dc, int j, unsigned long long seqj, double* rec_out) {
+    const bool sig = dc->xflag != nullptr;
+    if (sig) dc->xcount += (unsigned long long)dc->nf;   // one add per factor
+    if (dc->hdone) dc->slot_seq[j + 1] = seqj;
+    return exchange_and_copy(dc, j + 1, rec_out, sig);
+}
+
+// The deferred bookkeeping of the last one-sweep step as a k_post of its own.
+static tk_status bk_flush(tk_decomp* dc, double* rec_out) {
+    if (dc->bk_j < 0) return TK_OK;
+    tk_ctx* c = dc->ctx;
+    hipStream_t s = c->stream;
+    const int j = dc->bk_j;
+    const KArgs ax = dc->bk_args;
+    dc->bk_j = -1;
+    RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, ax, POST_ARN_D, 0, 1, s), "post");
+    return complete_step(dc, j, ax.seq, rec_out);
+}
+
+
 tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    tk_status st = slot_guard(dc, 0);
+    tk_status st = dc->failed ? TK_OK : bk_flush(dc);
+    if (st) return st;
+    dc->bk_j = -1;
+    st = slot_guard(dc, 0);
     if (st) return st;
     KArgs a = base_args(dc, 0, 0);
     const int nf = dc->nf;
@@ -1008,7 +1046,7 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
         } else {
             RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, f, s), "arn_finalize");
         }
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, np, s), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 3, j + 3, np, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, 1, s), "post");
     } else {
         if (fd) {
@@ -1043,7 +1081,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
         // overwritten by the CGS2 step below, which reports column j again)
-        tk_status st2 = finalize_pending(dc, base_args(dc, j - 1, slot));
+        tk_status st2 = bk_flush(dc);
+        if (st2) return st2;
+        st2 = finalize_pending(dc, base_args(dc, j - 1, slot));
         if (st2) return st2;
         dc->pending = false;
     }
@@ -1051,10 +1091,22 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // one sweep: writes v_j, u_{j+1}; reduce; post -> H column j and the next step's
         // coefficients.  v_j is re-derived from (U or W, h2, inv_beta) whether or not a
         // flush already wrote it (same operands, same order: the same value).
+        // The step's coefficients come from the previous step's reduced dots (d1_coef); the
+        // previous step's bookkeeping rides in a spare block of this launch, and this step's
+        // is deferred the same way (tk_decomp_step completes the previous step's record).
         a.ubuf = j & 1;
-        RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, dc->npd, s), "arn_d1");
-        if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s), "reduce");
-        if (!(dc->skip_mask & 2)) RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN_D, 0, 1, s), "post");
+        KArgs b = base_args(dc, -1, slot);
+        b.j = -1;
+        if (dc->bk_j >= 0 && dc->bk_j == j - 1) b = dc->bk_args;
+        else if (dc->bk_j >= 0) {
+            tk_status st2 = bk_flush(dc);
+            if (st2) return st2;
+        }
+        RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, s), "arn_d1");
+        // (its last block per factor also evaluates the next step's scalars)
+        if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
+        dc->bk_j = j;
+        dc->bk_args = ax;
         dc->pending = true;
     } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
@@ -1110,7 +1162,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s, 1), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, g, POST_ARN, 0, 0, s), "post");
         RUN(TCLS_FIN, 2, launch_arn_finalize(dc->df, nf, g, s), "arn_finalize");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 3, dc->npart, s, 1), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 3, j + 3, dc->npart, s, 1), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, g, POST_ARN_FIN, 0, 0, s), "post");
         // the record is final only after the gated redo: one ungated launch mirrors it to
         // the host (the exchange of a LanczosReorth handle waits on an event instead)
@@ -1129,7 +1181,8 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     if (j != dc->jnext) return fail(TK_ERR_STATE, "step %d requested, next step is %d", j, dc->jnext);
     if (j >= dc->kmax) return fail(TK_ERR_ARG, "step %d >= kmax %d", j, dc->kmax);
     HIPCHK(hipSetDevice(dc->ctx->device));
-    const bool sig = dc->xflag != nullptr;
+    const int prev_bk = dc->bk_j;
+    const unsigned long long prev_seq = dc->bk_args.seq;
     tk_status st = j == dc->fail_step ? fail(TK_ERR_HIP, "step %d: injected failure (TKHIP_TEST_FAIL_STEP)", j)
                                       : step_impl(dc, j, rec_out);
     if (st) {
@@ -1138,9 +1191,16 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
         dc->failed = true;
         return st;
     }
-    if (sig) dc->xcount += (unsigned long long)dc->nf;   // the step's k_post adds one per factor
-    if (dc->hdone) dc->slot_seq[j + 1] = dc->seq;
-    return exchange_and_copy(dc, j + 1, rec_out, sig);
+    if (dc->bk_j == j) {
+        // one sweep: this launch carried step j-1's bookkeeping (its record is complete);
+        // step j's own waits for the next launch unless the caller wants it now
+        if (prev_bk == j - 1 && prev_bk >= 0) {
+            st = complete_step(dc, prev_bk, prev_seq, nullptr);
+            if (st) return st;
+        }
+        return rec_out || !dc->bk_fold ? bk_flush(dc, rec_out) : TK_OK;
+    }
+    return complete_step(dc, j, dc->seq, rec_out);
     TK_API_END
 }
 
@@ -1153,6 +1213,7 @@ tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) { TK_API_BEGIN
     tk_status st = TK_OK;
     for (int j = j0; j < j1 && st == TK_OK; ++j) st = tk_decomp_step(dc, j, nullptr);
     dc->in_sweep = false;
+    if (st == TK_OK) st = bk_flush(dc);
     if (st == TK_OK) st = exchange_pending(dc);
     return st;
     TK_API_END
@@ -1162,6 +1223,10 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
     if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
     HIPCHK(hipSetDevice(dc->ctx->device));
+    {
+        tk_status st0 = bk_flush(dc);
+        if (st0) return st0;
+    }
     const int slot = dc->kmax + 1;
     if (!dc->pending) {
         if (rec_out) {
@@ -1187,6 +1252,10 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     HIPCHK(hipSetDevice(dc->ctx->device));
     const size_t per = (size_t)dc->d_total * dc->m;
     if (s1 == s0) return TK_OK;
+    if (dc->bk_j >= 0 && dc->bk_j + 1 >= s0 && dc->bk_j + 1 < s1 && !dc->failed) {
+        tk_status st = bk_flush(dc);
+        if (st) return st;
+    }
     if (dc->xp0 >= 0 && s1 - 1 >= dc->xp0) {
         tk_status st = exchange_pending(dc);
         if (st) return st;
@@ -1288,6 +1357,10 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
     tk_ctx* c = dc->ctx;
     HIPCHK(hipSetDevice(c->device));
     if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
+    {
+        tk_status st0 = bk_flush(dc);
+        if (st0) return st0;
+    }
     // a pending column is finalized first; for Arnoldi with the one-tile flush kernel it is
     // done in the same launch as V*Y (each basis tile streamed once for both)
     const int jl = dc->last_j;
@@ -1332,7 +1405,7 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
         KArgs f = a;
         if (dc->onesweep && jl <= D1_JMAX) f.ubuf = (jl & 1) ? 0 : 1;   // as finalize_pending
         RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, s), "fin_vy");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 1, jl + 3, dc->ntiles, s), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 3, jl + 3, dc->ntiles, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");
         dc->pending = false;
         st = exchange_and_copy(dc, slot, nullptr);

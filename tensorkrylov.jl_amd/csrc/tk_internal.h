@@ -64,6 +64,9 @@ struct DFac {
     // row windows of stride 256 - 2(hl+hu), window count, partial blocks (a function of
     // n, hl, hu only)
     int hl, hu, nwin, npd;
+    // one-sweep reduce: arrival counter of the step's value blocks (the last one evaluates
+    // the next step's scalars, k_reduce256)
+    unsigned int* ctr;
 };
 
 struct KArgs {
@@ -89,6 +92,15 @@ struct KArgs {
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
 // row); later steps of the same decomposition run as CGS2.
 constexpr int D1_JMAX = 64;
+// RED1 length: 3 kmax + 8 reduced values, plus the span one-sweep register rows read past
+// the live coefficients (2 x 64 + 16)
+#define RED1_LEN(kmax) (3 * (kmax) + 8 + 144)
+// where a one-sweep step's reduced dots (3j+6 values) are followed by the next step's
+// scalars (k_reduce256's last block): ib, gamma, beta, t1
+#define D1S_IB 0
+#define D1S_GAMMA 1
+#define D1S_BETA 2
+#define D1S_T1 3
 // 1: each k_arn_d1 block takes one window (DFac::npd == nwin); 0: blocks walk windows
 // (TKHIP_D1_WPB per block; 0 = about 1024 blocks per factor)
 #ifndef TK_D1_ONEWIN
@@ -106,7 +118,7 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s);   // j in 1..64
@@ -116,7 +128,8 @@ void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 // one partial per tile (reduce with npart = ntiles)
 void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s);
 // npart <= 0: each factor's own DFac::npd partials (one-sweep Arnoldi)
-void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0);
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0,
+                   int coefJ = -1);
 // post-processing (one 64-thread block per factor)
 enum PostKind {
     POST_INIT_A = 0,

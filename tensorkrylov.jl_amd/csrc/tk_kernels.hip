@@ -656,6 +656,10 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
 // sees bitwise the owner's values.  Only banded storage (hl, hu <= 4) takes this path.
 __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= TPB ? TPB - 1 : (int)i); }
 
+
+#ifndef TK_BK_TEST
+#define TK_BK_TEST 0
+#endif
 // occupancy by register-row width (measured at C2: 4 waves/SIMD up to 32 columns, 3 up
 // to 56; 40 columns at 4 waves spill)
 #ifndef TK_D1_L4
@@ -716,6 +720,8 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #else
 #define D1_PHASE(k) do { } while (0)
 #endif
+__device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds);
+__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored);
 template <int MAXC, int FMT>
 #ifndef TK_D1_OCCT
 #define TK_D1_OCCT 2
@@ -730,9 +736,10 @@ template <int MAXC, int FMT>
 #else
 #define D1_OCC OCC_WAVES(TK_D1_L4, TK_D1_L3)
 #endif
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a,
+                                                                                                  KArgs b) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
-    __shared__ double xs[4][TPB];   // v_j, u by window parity
+    __shared__ double xs[4][TPB];   // u_j, u_{j+1} by window parity
 #if TK_D1_COEF_LDS
     __shared__ __attribute__((aligned(16))) double cl[2][MAXC];   // c, h1
 #endif
@@ -743,7 +750,24 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // on XCD x % 8 (gridDim.x is a multiple of 8); each XCD takes a contiguous range of
     // windows -- neighbouring windows share halo rows in its L2 and its partial stores
     // fill whole lines there
-    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    // With the previous step's bookkeeping (b.j >= 0) the grid has 8 leading blocks (one per
+    // XCD, so the windows keep their XCD mapping); those of the first factor row run it for
+    // factors x, x+8, .. -- dispatched first, they finish while the windows stream (as
+    // trailing blocks they lengthened short launches by their own duration) -- and the window
+    // blocks do not wait for them.
+    const int x0 = b.j >= 0 ? 8 : 0;
+    if ((int)blockIdx.x < x0) {
+        if (blockIdx.y == 0 && !(TK_BK_TEST & 2))   // (TK_BK_TEST: timing experiments)
+            for (int f = blockIdx.x; f < (int)gridDim.y; f += 8) {
+                const DFac& df = F[f];
+                bk_arn_d(df, b, b.rec + (int64_t)df.gidx * b.m, lds);
+                if (!(TK_BK_TEST & 1)) post_signal(b, df, f, true);
+                __syncthreads();
+            }
+        return;
+    }
+    const int bx = (int)blockIdx.x - x0;
+    const int slot = (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
     if (slot >= d.nwin) return;
 #else
     if ((int)blockIdx.x >= d.npd) return;
@@ -758,10 +782,15 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const int hl = d.hl, hu = d.hu, WS = TPB - 2 * (hl + hu);
     const double* Uin = a.ubuf ? d.W : d.U;
     double* Uout = a.ubuf ? d.U : d.W;
-    const double inv_beta = ld(d.sc, SC_INVBETA);
+    // coefficients from the previous step's reduced dots (no post kernel in between):
+    // c = RED1[0, j), q = RED1[j, 2j), scalars after them (k_reduce256)
+#if TK_BK_TEST & 16
     const double* c = d.h2;
-    const double* h1 = d.g;
-    const double h1j = ld(d.g, j);
+    const double* qv = d.g;
+#else
+    const double* c = d.RED1;
+    const double* qv = d.RED1 + j;
+#endif
     const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
     const bool gram = d.track_gram != 0;
     const int nch = NUZ + 1 + (gram ? NG : 0);
@@ -771,7 +800,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // basis entries
     if (t < MAXC) {
         cl[0][t] = ld(c, t);
-        cl[1][t] = ld(h1, t);
+        cl[1][t] = ld(qv, t);
     }
     __syncthreads();
 #endif
@@ -793,20 +822,33 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         asm volatile("" : "+s"(jl));
         R.loadm(tv, toff, jl);
         const double up = inb ? ld(Uin, r) : 0.0;
-        double sc, sh;
+        // the step's scalars, evaluated by the last block of the previous step's reduce
+        // (k_reduce256): RED1 = [c (j) | q (j) | |u|^2, <u,z>, .. (3j+3 values) | ib, gamma, ..]
+        const double* s1 = d.RED1 + (j > 0 ? 3 * j + 3 : 2);
+        const double inv_beta = CP4(s1)[D1S_IB], gamma = CP4(s1)[D1S_GAMMA];
+        double sc, sq;
 #if TK_D1_COEF_LDS
-        row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sh);
+        row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sq);
 #else
-        row_dot2<MAXC>(R, c, h1, sc, sh);
+        row_dot2<MAXC>(R, c, qv, sc, sq);
 #endif
         D1_PHASE(0);
-        const double vj = ok ? (up - sc) * inv_beta : 0.0;
+        // v_j = (u_j - V c) ib.  With h1 = V'A v_j = (q - Hbar c) ib (CGS's first projection;
+        // q = V'A u_j from the previous sweep) and A v_j = (A u_j - A V c) ib, the Arnoldi
+        // relation A V c = V Hbar c turns CGS's
+        //   u_{j+1} = A v_j - V h1[0..j) - h1[j] v_j   into   ib (A u_j - V q) - gamma v_j
+        // (the Hbar c terms cancel): the SpMV is applied to u_j itself, no Hbar is needed
         double* xv = xs[par];
         double* xu = xs[2 + par];
+        const double vj = ok ? (up - sc) * inv_beta : 0.0;
+#if TK_BK_TEST & 32
         xv[t] = vj;
+#else
+        xv[t] = up;
+#endif
         __syncthreads();
-        const double av = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
-        const double u = ok ? av - (sh + h1j * vj) : 0.0;
+        const double au = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
+        const double u = ok ? inv_beta * (au - sq) - gamma * vj : 0.0;
         D1_PHASE(1);
         xu[t] = u;
         __syncthreads();
@@ -893,8 +935,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
         }
     }
-    // combine the 16 row-group partials of every value (fixed order) -> P1
-    //   [ p (c<j) | q (c<j) | p_j, q_j, |u|^2, <u,z>, <v_j,v_0>, gram_jj | gram (c<j) ]
+    // combine the row-group partials of every value (fixed order) -> P1, in the layout the
+    // next step reads its coefficients from (k_reduce256's last block, bk_arn_d)
+    //   [ c = p (c<=j) | q (c<=j) | |u|^2, <u,z>, <v_j,v_0>, gram_jj | gram (c<j) ]
     D1_PHASE(3);
     __syncthreads();
     for (int e = t; e < nch * 16; e += TPB) {
@@ -905,12 +948,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         int vi = -1;
         if (k < NUZ) {
             const int col = 8 * k + (sl >> 1);
-            if (col < j) vi = (sl & 1) ? j + col : col;
+            if (col < j) vi = (sl & 1) ? j + 1 + col : col;
         } else if (k == NUZ) {
 #if TK_D1_RS64 && TK_D1_SWPIN
-            if ((sl & 7) < 3) vi = 2 * j + (sl < 8 ? sl : sl - 5);   // slots 0,1,2 | 8,9,10
+            if ((sl & 7) < 3) vi = sl == 0 ? j : 2 * j + (sl < 8 ? sl : sl - 5);   // slots 0,1,2 | 8,9,10
 #else
-            if (sl < 6) vi = 2 * j + sl;
+            if (sl < 6) vi = sl == 0 ? j : 2 * j + sl;
 #endif
         } else {
 #if TK_D1_RS64 && TK_D1_SWPIN   // slot sl of Gram chunk g: pair q = sl & 3 of column chunk
@@ -1264,7 +1307,7 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
     if (c >= nv) return;
     if (gate && ld(d.sc, SC_REDO) == 0.0) return;
     if (npart <= 0) npart = d.npd;
-    const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
+    const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
     const int l = threadIdx.x;
     double s = 0.0;
     for (int b0 = 0; b0 < npart; b0 += 1024) {   // rounds of 16 independent loads per lane
@@ -1286,13 +1329,15 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 // Same for the one-sweep kernel's per-window partials (npart = DFac::npd, ~4k at n = 2^20):
 // four waves per value, each lane a strided subset in rounds of 16 independent loads, DPP
 // row sums, the 16 row totals summed in fixed order.
-__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np) {
+__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
+                                                   int coefJ) {
     __shared__ double rs[16];
+    __shared__ int last;
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
     if (c >= nv) return;
     const int npart = np > 0 ? np : d.npd;
-    const double* P = (which == 1 ? d.P1 : d.P2) + (int64_t)c * npart;
+    const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
     const int t = threadIdx.x;
     double s = 0.0;
     for (int b0 = 0; b0 < npart; b0 += 6144) {   // one round up to 6144 partials (n ~ 1.5M)
@@ -1312,7 +1357,48 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         double r = 0.0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) r += rs[q];
-        st(which == 1 ? d.RED1 : d.RED2, c, r);
+        if (coefJ < 0) {
+            st(which == 1 ? d.RED1 : d.RED2, c, r);
+        } else {
+            // one-sweep step: publish the value coherently (agent-scope store, through to the
+            // device-coherent level; its completion awaited), then count the arrival -- no
+            // L2 writeback.  The last of the nv blocks of this factor evaluates the scalars.
+            __hip_atomic_store(d.RED1 + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(0);
+            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
+        }
+    }
+    if (coefJ < 0) return;
+    __syncthreads();
+    if (!last || t >= 64) return;
+    // the next step's scalars from this step's dots (RED1 = c [0,J) | q [J,2J) | |u|^2 |
+    // <u,z> ..., J = coefJ <= 65): beta = sqrt(|u|^2 - |c|^2), ib = inv(beta),
+    // t1 = (<u,z> - c.q) ib, gamma = t1 ib = <v_J, A v_J> + (Hbar c)_J ib (the coefficient of
+    // v_J in u_{J+1}).  One wave, coherent loads, a fixed-order butterfly; k_arn_d1's blocks
+    // and the step's bookkeeping (bk_arn_d) read the results.
+    const int J = coefJ;
+    auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const double c0 = t < J ? cld(t) : 0.0, q0 = t < J ? cld(J + t) : 0.0;
+    const double c1 = t + 64 < J ? cld(t + 64) : 0.0, q1 = t + 64 < J ? cld(J + 64 + t) : 0.0;
+    const double uu = cld(2 * J), uz = cld(2 * J + 1);
+    double cc = fma(c1, c1, c0 * c0), cq = fma(c1, q1, c0 * q0);
+    cc = row16_sum(cc);
+    cc += __shfl_xor(cc, 16);
+    cc += __shfl_xor(cc, 32);
+    cq = row16_sum(cq);
+    cq += __shfl_xor(cq, 16);
+    cq += __shfl_xor(cq, 32);
+    if (t == 0) {
+        const double bsq = uu - cc;
+        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+        const double ib = 1.0 / beta;
+        const double t1 = (uz - cq) * ib;
+        double* o = d.RED1 + nv;
+        st(o, D1S_IB, ib);
+        st(o, D1S_GAMMA, t1 * ib);
+        st(o, D1S_BETA, beta);
+        st(o, D1S_T1, t1);
+        __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1411,130 +1497,99 @@ __device__ void post_arn(const DFac& d, const KArgs& a, double* rec, const doubl
     put_gram(rec, kmax, j, red2 + j + 3, red2[j + 2], d.track_gram);
 }
 
-// One-sweep Arnoldi post-processing of step j.  RED1 holds (k_arn_d1)
-//   p = <V[:,c],u> (c<j) | q = <V[:,c],z> (c<j) | p_j, q_j, |u|^2, <u,z>, <v_j,v_0>, gram_jj |
-//   gram (c<j)
-// with u = u_{j+1}, z = A u; bt_j = norm(b) <v_j,v_0>.  The reorthogonalization coefficients of u are c = p; then
-//   H[0..j, j] = h1 + c,  beta = H[j+1, j] = sqrt(|u|^2 - |c|^2)        (CGS2 of
+// Bookkeeping of one-sweep Arnoldi step j (a.j): everything the host and the later kernels
+// read, none of which the next step's blocks wait for (they derive their coefficients from
+// RED1 and the scalars k_reduce256 appends).  RED1 holds step j's reduced dots (k_arn_d1's layout)
+//   c = <V[:,i],u> (i<=j) | q = <V[:,i],z> (i<=j) | |u|^2, <u,z>, <v_j,v_0>, gram_jj | gram (i<j)
+// with u = u_{j+1}, z = A u.  c are the reorthogonalization coefficients of u, so
+//   H[0..j, j] = h1 + c,  beta = H[j+1, j] = sqrt(|u|^2 - |c|^2)   (CGS2 of
 //   src/orthogonal_bases.jl:22-36 in exact arithmetic),  v_{j+1} = (u - V c) * inv(beta),
-// and the first projection of A v_{j+1} = (z - V Hbar c) * inv(beta) (Arnoldi relation for
-// the small correction A V c) follows from the sweep's dots with V'V = I, V'v_{j+1} = 0:
+// with h1 = d.g the first projection of A v_j (from the previous bookkeeping).  The first
+// projection of A v_{j+1} = (z - A V c) * inv(beta) = (z - V Hbar c) * inv(beta) follows from
+// the sweep's dots with V'V = I, V'v_{j+1} = 0:
 //   h1'[l] = (q_l - (Hbar c)_l) * inv(beta)   (l <= j)
 //   h1'[j+1] = ((<u,z> - c.q) * inv(beta) - (Hbar c)_{j+1}) * inv(beta)
-// c -> h2, h1' -> g (the next sweep's coefficients), inv(beta) -> scalars, the step's
-// record (H column j, beta, bt_j and the Gram row of column j).
-__device__ void post_arn_d(const DFac& d, const KArgs& a, double* rec, double* Hs, double* red, double* h1s,
-                           double* row, double* sh) {
+// c -> h2, inv(beta) -> scalars (the flush of the pending column reads them), h1' -> d.g,
+// and the step's record row (H column j, beta, bt_j = norm(b) <v_j,v_0>, the Gram row of
+// column j) with its host mirror -- every entry written once.  lds: Hbar ((j+1)(j+2)
+// doubles, j <= 64) then the reduced dots (3j+6).
+__device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds) {
     const int j = a.j, kmax = a.kmax;
     const int t = threadIdx.x;
     double* Hc = d.H + (int64_t)j * (kmax + 2);
     const int J2 = j + 2, nv = 3 * j + 6;
-    // every global load of the kernel in one round trip: Hbar[:, 0..j) (16 per thread in
-    // flight; j <= 64 fits), the reduced dots, the current h1 and norm(b).  The record row is
-    // assembled in LDS (row) and written out once.
-    // (a wave per column, a lane per row: no index division; columns i, i+4, ... of a wave
-    // in flight together)
-    {
-        const int w = t >> 6, ln = t & 63;
-        for (int l0 = 0; l0 < J2; l0 += 64) {
-            const int l = l0 + ln;
-            for (int i0 = 0; i0 < j; i0 += 64) {
-                double hv[16];
+    double* Hs = lds;
+    double* red = lds + (((j + 1) * J2 + 1) & ~1);
+    // Hbar[:, 0..j) eight loads in flight per thread (few registers: this also runs in a
+    // spare block of k_arn_d1, whose register budget is the window blocks'), the reduced
+    // dots and h1 (column j of Hs until + c)
+    const int HN = j * J2;
+    for (int e0 = 0; e0 < HN; e0 += 8 * TPB) {
+        double hv[8];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int i = i0 + 4 * q + w;
-                    hv[q] = (i < j && l <= i + 1) ? ld(d.H, (int64_t)i * (kmax + 2) + l) : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int i = i0 + 4 * q + w;
-                    if (i < j && l < J2) Hs[i * J2 + l] = hv[q];
-                }
-            }
+        for (int q = 0; q < 8; ++q) {
+            const int e = e0 + q * TPB + t;
+            const int i = e / J2, l = e - i * J2;
+            hv[q] = (e < HN && l <= i + 1) ? ld(d.H + (int64_t)i * (kmax + 2), l) : 0.0;
         }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (e0 + q * TPB + t < HN) Hs[e0 + q * TPB + t] = hv[q];
     }
     for (int i = t; i < nv; i += TPB) red[i] = ld(d.RED1, i);
-    for (int i = t; i <= j; i += TPB) h1s[i] = ld(d.g, i);
-    for (int i = t; i < a.m; i += TPB) row[i] = 0.0;
-    if (t == 0) sh[10] = ld(d.sc, SC_BNORM);
+    for (int i = t; i <= j; i += TPB) Hs[j * J2 + i] = ld(d.g, i);
+    const double bnorm = ld(d.sc, SC_BNORM);
+    const double beta = ld(d.RED1, nv + D1S_BETA), ib = ld(d.RED1, nv + D1S_IB), t1 = ld(d.RED1, nv + D1S_T1);
     __syncthreads();
-    // c (p_l, l < j, then p_j) and q likewise
-    const double* cp = red;
-    const double* qp = red + j;
-    double cc = 0.0, cq = 0.0;
     for (int i = t; i <= j; i += TPB) {
-        const double ci = i < j ? cp[i] : red[2 * j];
-        const double qi = i < j ? qp[i] : red[2 * j + 1];
-        const double hv = h1s[i] + ci;
+        const double ci = red[i];
+        const double hv = Hs[j * J2 + i] + ci;
         st(Hc, i, hv);
         st(d.h2, i, ci);
-        row[i] = hv;
         Hs[j * J2 + i] = hv;
-        h1s[i] = ci;   // c, for the Hbar c products below
-        cc += ci * ci;
-        cq += ci * qi;
     }
-    cc = row16_sum(cc);
-    cc += __shfl_xor(cc, 16);
-    cc += __shfl_xor(cc, 32);
-    cq = row16_sum(cq);
-    cq += __shfl_xor(cq, 16);
-    cq += __shfl_xor(cq, 32);
-    if ((t & 63) == 0) {
-        sh[t >> 6] = cc;
-        sh[4 + (t >> 6)] = cq;
-    }
-    __syncthreads();
     if (t == 0) {
-        const double s2 = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-        const double bsq = red[2 * j + 2] - s2;
-        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
         st(Hc, j + 1, beta);
         Hs[j * J2 + j + 1] = beta;
-        row[j + 1] = beta;
-        row[rec_beta(kmax)] = beta;
         st(d.sc, SC_BETA, beta);
-        st(d.sc, SC_INVBETA, 1.0 / beta);
+        st(d.sc, SC_INVBETA, ib);
         st(d.sc, SC_BETAPREV, beta);
-        sh[8] = beta;
-        sh[9] = (sh[4] + sh[5]) + (sh[6] + sh[7]);
-        row[rec_bt(kmax)] = sh[10] * red[2 * j + 4];   // norm(b) <v_j, v_0>
-        row[rec_col(kmax)] = (double)j;
-        row[rec_tracked(kmax)] = d.track_gram ? 1.0 : 0.0;
     }
-    // Gram row of column j: [gram (c<j), gram_jj]
-    if (d.track_gram)
-        for (int i = t; i <= j; i += TPB) row[rec_gram(kmax) + i] = i < j ? red[2 * j + 6 + i] : red[2 * j + 5];
     __syncthreads();
     // h1'[l] from (Hbar c)_l: four lanes per l over interleaved i, combined in fixed order
-    const double beta = sh[8], ib = 1.0 / beta;
     for (int l0 = 0; l0 <= j + 1; l0 += TPB / 4) {
         const int l = l0 + (t >> 2), r = t & 3;
         double sum = 0.0;
         if (l <= j + 1)
-            for (int i = (l > 0 ? l - 1 : 0) + r; i <= j; i += 4) sum += Hs[i * J2 + l] * h1s[i];
+            for (int i = (l > 0 ? l - 1 : 0) + r; i <= j; i += 4) sum += Hs[i * J2 + l] * red[i];
         sum += __shfl_xor(sum, 1);
         sum += __shfl_xor(sum, 2);
-        if (r == 0 && l <= j + 1) {
-            const double h = l <= j ? ((l < j ? qp[l] : red[2 * j + 1]) - sum) * ib
-                                    : ((red[2 * j + 3] - sh[9]) * ib - sum) * ib;
-            st(d.g, l, h);
-        }
+        if (r == 0 && l <= j + 1) st(d.g, l, l <= j ? (red[j + 1 + l] - sum) * ib : (t1 - sum) * ib);
     }
-    __syncthreads();
-    // the record row, and its host mirror
+    // the record row (zeros included) and its host mirror
     double* hr = a.hdone ? a.hrec + (int64_t)d.gidx * a.m : nullptr;
+    const int g0 = rec_gram(kmax);
     for (int i = t; i < a.m; i += TPB) {
-        st(rec, i, row[i]);
-        if (hr) hr[i] = row[i];
+        double v = 0.0;
+        if (i <= j + 1) v = Hs[j * J2 + i];
+        else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? red[2 * j + 6 + i - g0] : red[2 * j + 5]) : 0.0;
+        else if (i == rec_beta(kmax)) v = beta;
+        else if (i == rec_bt(kmax)) v = bnorm * red[2 * j + 4];   // norm(b) <v_j, v_0>
+        else if (i == rec_col(kmax)) v = (double)j;
+        else if (i == rec_tracked(kmax)) v = d.track_gram ? 1.0 : 0.0;
+        st(rec, i, v);
+        if (hr) hr[i] = v;
     }
+}
+__host__ __device__ inline size_t bk_lds_doubles(int j) {
+    return (size_t)((((j + 1) * (j + 2) + 1) & ~1) + 3 * j + 10);
 }
 
 // Tell the exchange stream that this block's record row is complete: all threads' stores
 // are ordered before thread 0's device-scope release, then one system-scope add to the
 // signal word (the stream waits for the count of all of the step's blocks; no event marker
 // in the compute queue).
-__device__ __forceinline__ void post_signal(const KArgs& a, const DFac& d, bool mirrored = false) {
+__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored) {
     if (!a.xflag && !a.hdone) return;
     __syncthreads();
     if (a.hdone && !mirrored) {
@@ -1550,7 +1605,7 @@ __device__ __forceinline__ void post_signal(const KArgs& a, const DFac& d, bool 
         __threadfence_system();
         if (a.xflag) atomicAdd_system(a.xflag, 1ull);
         if (a.hdone)
-            __hip_atomic_store(a.hdone + blockIdx.x, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(a.hdone + fidx, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1558,13 +1613,11 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
                                               int clear) {
     __shared__ double sh[16];
     __shared__ double h2s[1024 + 8];
-    __shared__ double qs[1024 + 8];
-    __shared__ double h1s[1024 + 8];
     extern __shared__ __attribute__((aligned(16))) double post_lds[];
     const DFac& d = F[blockIdx.x];
     if (a.gate && ld(d.sc, SC_REDO) == 0.0) return;
     if (kind == POST_SIGNAL) {
-        post_signal(a, d);
+        post_signal(a, d, (int)blockIdx.x, false);
         return;
     }
     const int j = a.j, kmax = a.kmax;
@@ -1582,6 +1635,9 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
             st(d.g, i, 0.0);
         }
         for (int i = t + 1; i < 2 * kmax + 8; i += TPB) st(d.RED2, i, 0.0);
+        // (one-sweep register rows read RED1 past the live coefficients, against zero basis
+        // entries: nothing stale from an earlier solve may be non-finite there)
+        for (int i = t + 1; i < RED1_LEN(kmax); i += TPB) st(d.RED1, i, 0.0);
         if (t == 0) {
             const double nrm = sqrt(ld(d.RED1, 0));
             st(d.sc, SC_BNORM, nrm);
@@ -1592,30 +1648,41 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_INIT_B) {
         put_gram(rec, kmax, 0, d.RED1 + 1, ld(d.RED1, 0), d.track_gram);
         if (t == 0 && d.track_gram) st(d.lossrow, 0, loss_row(d.RED1 + 1, 0));
-        if (t == 0 && flag) {
-            // one-sweep Arnoldi: step 0 re-derives v_0 = U * 1.0 with no coefficients;
-            // h1 = [<v0, A v0>]
-            st(d.g, 0, ld(d.RED1, 2));
-            st(d.sc, SC_INVBETA, 1.0);
+        if (flag) {
+            // one-sweep Arnoldi: step 0 re-derives v_0 = U * 1.0 with no coefficients: its
+            // scalars are beta = ib = 1 and gamma = <v0, A v0> (after the 3 init values), and
+            // the bookkeeping's h1 = [<v0, A v0>]
+            __syncthreads();   // (the record reads of RED1 above are done)
+            if (t == 0) {
+                const double vav = ld(d.RED1, 2);
+                st(d.g, 0, vav);
+                st(d.sc, SC_INVBETA, 1.0);
+                double* o = d.RED1 + 2;   // (k_arn_d1 step 0 reads its scalars here)
+                st(o, D1S_IB, 1.0);
+                st(o, D1S_GAMMA, vav);
+                st(o, D1S_BETA, 1.0);
+                st(o, D1S_T1, vav);
+            }
         }
         return;
     }
     if (kind == POST_ARN) {
         double* Hs = (a.kmax + 1) * (a.kmax + 2) <= POST_LDS_MAX ? post_lds : nullptr;   // = launcher's size
         post_arn(d, a, rec, d.RED1, d.RED2, Hs, h2s, sh);
-        post_signal(a, d);
+        post_signal(a, d, (int)blockIdx.x, false);
         return;
     }
     if (kind == POST_ARN_D) {
-        // dynamic LDS: Hbar ((j+1)(j+2) doubles, j <= 64), then the record row (m)
-        post_arn_d(d, a, rec, post_lds, qs, h1s, post_lds + (((a.j + 1) * (a.j + 2) + 1) & ~1), sh);
-        post_signal(a, d, true);
+        // dynamic LDS: Hbar ((j+1)(j+2) doubles, j <= 64), then the reduced dots
+        bk_arn_d(d, a, rec, post_lds);
+        post_signal(a, d, (int)blockIdx.x, true);
         return;
     }
     if (kind == POST_ARN_FIN) {
-        // RED1 = [gram_{j+1} (j+2) | bt]
-        put_gram(rec, kmax, j + 1, d.RED1, ld(d.RED1, j + 2), d.track_gram);
-        if (t == 0 && d.track_gram) st(d.lossrow, j + 1, loss_row(d.RED1, j + 1));   // (redone column)
+        // RED2 = [gram_{j+1} (j+2) | bt] (reduced from P1 into RED2: RED1 keeps the one-sweep
+        // step's dots, which the next step still reads)
+        put_gram(rec, kmax, j + 1, d.RED2, ld(d.RED2, j + 2), d.track_gram);
+        if (t == 0 && d.track_gram) st(d.lossrow, j + 1, loss_row(d.RED2, j + 1));   // (redone column)
         return;
     }
     if (kind == POST_LAN) {
@@ -1632,7 +1699,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
         }
         if (flag) put_gram(rec, kmax, j, d.RED1 + 2, ld(d.RED1, 1), d.track_gram);
         else if (t == 0) st(rec, rec_col(kmax), -1.0);
-        post_signal(a, d);
+        post_signal(a, d, (int)blockIdx.x, false);
         return;
     }
     if (kind == POST_LAN_FIN) {
@@ -1869,15 +1936,17 @@ void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t 
         hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
     });
 }
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
-    // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
+    // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
+    // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
-    const size_t lds = (size_t)(M / 8 + 1 + (M + 15) / 16) * TPB * sizeof(double);
+    size_t lds = (size_t)(M / 8 + 1 + (M + 15) / 16) * TPB * sizeof(double);
+    if (b.j >= 0) lds = std::max(lds, bk_lds_doubles(b.j) * sizeof(double));
+    const int gx = TK_D1_ONEWIN ? (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
     with_band_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
-            hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value>),
-                               dim3(TK_D1_ONEWIN ? (npd + 7) / 8 * 8 : npd, nf), dim3(TPB),
-                               lds, s, F, a);
+            hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value>), dim3(gx, nf), dim3(TPB),
+                               lds, s, F, a, b);
         });
     });
 }
@@ -1928,11 +1997,11 @@ void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, doubl
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
-void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate) {
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ) {
     if (npart <= 0 && !gate)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0);
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ);
     else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart);
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1);
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }
@@ -1956,7 +2025,7 @@ void launch_mirror_records(const double* src, double* dst, int cnt, unsigned lon
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
     size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
-    if (kind == POST_ARN_D) lds = (size_t)((((a.j + 1) * (a.j + 2) + 1) & ~1) + a.m) * sizeof(double);
+    if (kind == POST_ARN_D) lds = bk_lds_doubles(a.j) * sizeof(double);
     hipLaunchKernelGGL(k_post, dim3(nf), dim3(TPB), lds, s, F, a, kind, flag, clear);
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,

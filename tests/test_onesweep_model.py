@@ -1,11 +1,16 @@
 """CPU model of the device's one-sweep Arnoldi (CGS2 with the
 reorthogonalization delayed one step) against the MGS2 oracle (src/orthogonal_bases.jl:15-37).
 
-The model restates, column by column and in exact correspondence with k_arn_d1 + post_arn_d
-(tensorkrylov.jl_amd/csrc/tk_kernels.hip), the recurrences the GPU evaluates row-wise:
-  v_j = (u_j - V c) / beta_j;  u_{j+1} = A v_j - V h1;  z = A u_{j+1};
-  c' = V' u;  beta' = sqrt(|u|^2 - |c'|^2);  H[:, j] = h1 + c';
-  h1' = [(q - Hbar c') / beta' ; ((<u,z> - c'.q) / beta' - (Hbar c')_{j+1}) / beta'].
+The model restates, column by column and in exact correspondence with k_arn_d1 + d1_coef +
+bk_arn_d (tensorkrylov.jl_amd/csrc/tk_kernels.hip), the recurrences the GPU evaluates
+row-wise.  Step J takes its coefficients straight from step J-1's dots
+(c = V'u_J, q = V'A u_J, |u_J|^2, <u_J, A u_J>):
+  beta = sqrt(|u|^2 - |c|^2);  gamma = (<u,Au> - c.q) / beta^2;
+  v_J = (u_J - V c) / beta;    u_{J+1} = (A u_J - V q) / beta - gamma v_J
+(CGS's u_{J+1} = A v_J - V h1 with h1 = (q - Hbar c) / beta, after the Arnoldi relation
+A V c = V Hbar c cancels the Hbar terms).  The record of step J-1 (bookkeeping, off the
+device's critical path) keeps the explicit first projection:
+  H[:, J-1] = h1 + c;  h1' = [(q - Hbar c) / beta ; (<u,Au> - c.q) / beta^2 - (Hbar c)_J / beta].
 It pins the algorithm's numerics independently of the GPU: H and V agree with MGS2 to the
 parity tolerance of the GPU tests (1e-12 relative) -- and to ~1e-15 in practice -- for the
 gallery's Laplace and convection-diffusion matrices, up to k close to n."""
@@ -22,23 +27,29 @@ def onesweep_arnoldi(A, b, K):
     H = np.zeros((K + 2, K + 1))
     v0 = (1.0 / np.linalg.norm(b)) * b
     V[:, 0] = v0
-    U, c, invb = v0.copy(), np.zeros(0), 1.0            # k_init_bd / POST_INIT_B
-    h1 = np.array([v0 @ (A @ v0)])
-    for j in range(K):                                   # k_arn_d1 step j
-        vj = (U - V[:, :j] @ c) * invb
-        V[:, j] = vj
-        u = A @ vj - V[:, :j + 1] @ h1
+    U = v0.copy()                                        # k_init_bd / POST_INIT_B:
+    c, q, uu, uz = np.zeros(0), np.zeros(0), 1.0, v0 @ (A @ v0)   # beta = 1, gamma = <v0,Av0>
+    h1 = np.array([uz])
+    for J in range(K):                                   # k_arn_d1 step J
+        beta = np.sqrt(max(uu - c @ c, 0.0))             # d1_coef
+        ib = 1.0 / beta
+        t1 = (uz - c @ q) * ib
+        gamma = t1 * ib
+        if J >= 1:                                       # bk_arn_d of step J-1
+            H[:J, J - 1] = h1 + c
+            H[J, J - 1] = beta
+            g = H[:J + 1, :J] @ c
+            h1 = np.concatenate([(q - g[:J]) * ib, [(t1 - g[J]) * ib]])
+        vj = (U - V[:, :J] @ c) * ib
+        V[:, J] = vj
+        u = ib * (A @ U - V[:, :J] @ q) - gamma * vj
         z = A @ u
-        p, q = V[:, :j + 1].T @ u, V[:, :j + 1].T @ z
-        uu, uz = u @ u, u @ z
-        c = p                                            # post_arn_d
-        beta = np.sqrt(max(uu - p @ p, 0.0))
-        H[:j + 1, j] = h1 + c
-        H[j + 1, j] = beta
-        g = H[:j + 2, :j + 1] @ c
-        h1 = np.concatenate([(q - g[:j + 1]) / beta, [((uz - c @ q) / beta - g[j + 1]) / beta]])
-        U, invb = u, 1.0 / beta
-    V[:, K] = (U - V[:, :K] @ c) * invb                  # k_arn_finalize (flush)
+        c, q, uu, uz = V[:, :J + 1].T @ u, V[:, :J + 1].T @ z, u @ u, u @ z
+        U = u
+    beta = np.sqrt(max(uu - c @ c, 0.0))                 # bk_arn_d of step K-1 + the flush
+    H[:K, K - 1] = h1 + c
+    H[K, K - 1] = beta
+    V[:, K] = (U - V[:, :K] @ c) * (1.0 / beta)
     return V, H
 
 
