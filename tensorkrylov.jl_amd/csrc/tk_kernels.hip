@@ -721,7 +721,7 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #define D1_PHASE(k) do { } while (0)
 #endif
 __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds);
-__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored);
+__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent = false);
 template <int MAXC, int FMT>
 #ifndef TK_D1_OCCT
 #define TK_D1_OCCT 2
@@ -761,7 +761,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             for (int f = blockIdx.x; f < (int)gridDim.y; f += 8) {
                 const DFac& df = F[f];
                 bk_arn_d(df, b, b.rec + (int64_t)df.gidx * b.m, lds);
-                if (!(TK_BK_TEST & 1)) post_signal(b, df, f, true);
+                if (!(TK_BK_TEST & 1)) post_signal(b, df, f, true, true);
                 __syncthreads();
             }
         return;
@@ -1577,8 +1577,10 @@ __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds
         else if (i == rec_bt(kmax)) v = bnorm * red[2 * j + 4];   // norm(b) <v_j, v_0>
         else if (i == rec_col(kmax)) v = (double)j;
         else if (i == rec_tracked(kmax)) v = d.track_gram ? 1.0 : 0.0;
-        st(rec, i, v);
-        if (hr) hr[i] = v;
+        // (post_signal: stores through to the coherence level the readers use -- the device's
+        // for the exchange's all-reduce, the system's for the host mirror)
+        __hip_atomic_store(rec + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hr) __hip_atomic_store(hr + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 __host__ __device__ inline size_t bk_lds_doubles(int j) {
@@ -1589,8 +1591,22 @@ __host__ __device__ inline size_t bk_lds_doubles(int j) {
 // are ordered before thread 0's device-scope release, then one system-scope add to the
 // signal word (the stream waits for the count of all of the step's blocks; no event marker
 // in the compute queue).
-__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored) {
+// coherent: the block wrote its record row with agent-scope stores (through to the device-
+// coherent level, what the exchange stream's all-reduce reads) and its host mirror with
+// system-scope stores (through to host memory), so each thread's completed stores
+// (s_waitcnt) are all the signal must follow -- no system-scope fence, whose L2 writeback
+// stalls the kernels running beside this block.
+__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent) {
     if (!a.xflag && !a.hdone) return;
+    if (coherent) {
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (a.xflag) __hip_atomic_fetch_add(a.xflag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.hdone) __hip_atomic_store(a.hdone + fidx, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
     __syncthreads();
     if (a.hdone && !mirrored) {
         // host mirror of the record row (host-mapped, coherent), then its sequence number:
@@ -1675,7 +1691,7 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
     if (kind == POST_ARN_D) {
         // dynamic LDS: Hbar ((j+1)(j+2) doubles, j <= 64), then the reduced dots
         bk_arn_d(d, a, rec, post_lds);
-        post_signal(a, d, (int)blockIdx.x, true);
+        post_signal(a, d, (int)blockIdx.x, true, true);
         return;
     }
     if (kind == POST_ARN_FIN) {
@@ -2010,12 +2026,15 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
 // their sequence number, so the host reads the records without any queue call.
 __global__ __launch_bounds__(TPB) void k_mirror_records(const double* __restrict__ src, double* dst, int cnt,
                                                         unsigned long long* done, int nslots, unsigned long long seq) {
-    for (int i = threadIdx.x; i < cnt; i += TPB) dst[i] = ld(src, i);
+    // (system-scope stores go through to host memory: each thread's completed stores are all
+    // the sequence words must follow; no system-scope fence and its L2 writeback beside the
+    // compute kernels)
+    for (int i = threadIdx.x; i < cnt; i += TPB)
+        __hip_atomic_store(dst + i, ld(src, i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        for (int q = 0; q < nslots; ++q) __hip_atomic_store(done + q, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (threadIdx.x == 0)
+        for (int q = 0; q < nslots; ++q) __hip_atomic_store(done + q, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
                            unsigned long long seq, hipStream_t s) {
