@@ -729,6 +729,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.H, (size_t)KP * KC * sizeof(double));
         DA(d.lossrow, (size_t)KP * sizeof(double));
         DA(d.ctr, 16);
+        DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
@@ -886,6 +887,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.hrec = nullptr;
     a.hdone = nullptr;
     a.seq = 0;
+    a.ecol = -1;
     return a;
 }
 
@@ -1040,7 +1042,10 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
     const int np = fd ? dc->ntiles : dc->npart;
     if (dc->method == TK_ARNOLDI) {
         KArgs f = a;
-        if (dc->onesweep && j <= D1_JMAX) f.ubuf = (j & 1) ? 0 : 1;   // one-sweep step j wrote u_{j+1} to U (j odd) or W
+        if (dc->onesweep && j <= ARN_D1_JMAX) {
+            f.ubuf = (j & 1) ? 0 : 1;   // one-sweep step j wrote u_{j+1} to U (j odd) or W
+            f.ecol = (j & 1) ? -1 : j;  // ... and an even v_j to E
+        }
         if (fd) {
             RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, f, 0, s), "fin_d");
         } else {
@@ -1078,7 +1083,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         ax.seq = ++dc->seq;
     }
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
-    if (dc->method == TK_ARNOLDI && dc->onesweep && j > D1_JMAX && dc->pending && dc->last_j <= D1_JMAX) {
+    if (dc->method == TK_ARNOLDI && dc->onesweep && j > ARN_D1_JMAX && dc->pending && dc->last_j <= ARN_D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
         // overwritten by the CGS2 step below, which reports column j again)
         tk_status st2 = bk_flush(dc);
@@ -1087,7 +1092,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         if (st2) return st2;
         dc->pending = false;
     }
-    if (dc->method == TK_ARNOLDI && dc->onesweep && j <= D1_JMAX) {
+    if (dc->method == TK_ARNOLDI && dc->onesweep && j <= ARN_D1_JMAX) {
         // one sweep: writes v_j, u_{j+1}; reduce; post -> H column j and the next step's
         // coefficients.  v_j is re-derived from (U or W, h2, inv_beta) whether or not a
         // flush already wrote it (same operands, same order: the same value).
@@ -1327,7 +1332,10 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     CHECKARG(f >= 0 && f < dc->nf, "factor out of range");
     CHECKARG(c0 >= 0 && nc >= 0 && c0 + nc <= dc->kmax + 1, "column range");
     HIPCHK(hipSetDevice(dc->ctx->device));
-    if (dc->pending && c0 + nc - 1 > dc->last_j) {
+    // (one-sweep Arnoldi after an even step: column last_j is still in DFac::E; the flush
+    // stores it with the pending column)
+    const bool in_e = dc->method == TK_ARNOLDI && dc->onesweep && dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
+    if (dc->pending && nc > 0 && c0 + nc - 1 >= dc->last_j + (in_e ? 0 : 1)) {
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;
     }
@@ -1403,7 +1411,10 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
         if (st) return st;
         KArgs a = base_args(dc, jl, slot);
         KArgs f = a;
-        if (dc->onesweep && jl <= D1_JMAX) f.ubuf = (jl & 1) ? 0 : 1;   // as finalize_pending
+        if (dc->onesweep && jl <= ARN_D1_JMAX) {   // as finalize_pending
+            f.ubuf = (jl & 1) ? 0 : 1;
+            f.ecol = (jl & 1) ? -1 : jl;
+        }
         RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, s), "fin_vy");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 3, jl + 3, dc->ntiles, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");

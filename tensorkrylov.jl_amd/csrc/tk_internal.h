@@ -64,6 +64,9 @@ struct DFac {
     // row windows of stride 256 - 2(hl+hu), window count, partial blocks (a function of
     // n, hl, hu only)
     int hl, hu, nwin, npd;
+    // one-sweep Arnoldi: the even column written by the last even step (v_j, n rows); the
+    // odd step after it stores the pair (v_{j-1}, v_j) once, so no column is written twice
+    double* E;
     // one-sweep reduce: arrival counter of the step's value blocks (the last one evaluates
     // the next step's scalars, k_reduce256)
     unsigned int* ctr;
@@ -87,11 +90,15 @@ struct KArgs {
                                  // ([d_total][m]); k_post copies its row there ...
     unsigned long long* hdone;   // ... then stores `seq` to hdone[local factor] (host-mapped)
     unsigned long long seq;
+    int ecol;         // flush of the one-sweep pending column: this column (j) is in DFac::E, not V (-1: none)
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
 // row); later steps of the same decomposition run as CGS2.
 constexpr int D1_JMAX = 64;
+// the one-sweep Arnoldi runs steps j <= ARN_D1_JMAX: its last step is odd, so leaving the
+// range never leaves an even column in DFac::E (the CGS2 kernels read V only)
+constexpr int ARN_D1_JMAX = 63;
 // RED1 length: 3 kmax + 8 reduced values, plus the span one-sweep register rows read past
 // the live coefficients (2 x 64 + 16)
 #define RED1_LEN(kmax) (3 * (kmax) + 8 + 144)

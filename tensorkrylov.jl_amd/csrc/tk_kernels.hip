@@ -230,18 +230,43 @@ struct Row {
         }
         if (nc > MAXC) last = bld(tile, toff + cofs(nc - 1));
     }
-    // Same through a resource over the factor's whole basis (rows of two tiles in one
-    // wave): pairs past nc are skipped (wave-uniform), not range-checked.  Rows outside
-    // the basis pass toff >= 2^31, beyond the resource: every load returns zero.
-    // The caller sizes the row to the step (MAXC - 8 < nc <= MAXC, or MAXC == 8): only the
-    // last four pairs need the uniform column checks, and `last` is one of their columns.
+    // Column c (MAXC - 8 <= c < MAXC, or MAXC == 8; wave-uniform; loaded as zero) := x, and
+    // `last` := x.  Masked adds, not a conditional store: that one the compiler merged into
+    // a dynamically indexed store and moved the whole row to scratch.
+    __device__ __forceinline__ void set_col(int c, double x) {
+        constexpr int C0 = MAXC > 8 ? MAXC - 8 : 0;
+        const uint64_t xb = __builtin_bit_cast(uint64_t, x);
+#pragma unroll
+        for (int q = C0; q < MAXC; ++q)
+            v[q] += __builtin_bit_cast(double, xb & (0ull - (uint64_t)(q == c)));
+        last = x;
+    }
+    // Same as load through a resource over the factor's whole basis (rows of two tiles in
+    // one wave): pairs past nc get an offset beyond the resource, like rows outside the
+    // basis (toff >= 2^31): every such load returns zero.  The caller sizes the row to the
+    // step (MAXC - 8 <= nc <= MAXC, or MAXC == 8): only the last four pairs need the uniform
+    // column checks, and `last` is one of their columns.
+    // loadm for an even nc: whole pairs only, no selects on the loaded values (a uniform
+    // select there made the compiler wait for the row before its next loads); `last` unset
+    __device__ __forceinline__ void loadm_even(rsrc_t basis, uint32_t toff, int nc) {
+        constexpr int P0 = MAXC / 2 - 4;
+#pragma unroll
+        for (int p = 0; p < MAXC / 2; ++p) {
+            const uint32_t off = (p < P0 || 2 * p < nc) ? toff + (uint32_t)p * (TPB * 16) : 0x80000000u;
+            const d2_t x = bld2(basis, off);
+            v[2 * p] = x.x;
+            v[2 * p + 1] = x.y;
+        }
+    }
     __device__ __forceinline__ void loadm(rsrc_t basis, uint32_t toff, int nc) {
         constexpr int P0 = MAXC / 2 - 4;
         last = 0.0;
 #pragma unroll
         for (int p = 0; p < MAXC / 2; ++p) {
-            d2_t x = (d2_t){0.0, 0.0};
-            if (p < P0 || 2 * p < nc) x = bld2(basis, toff + (uint32_t)p * (TPB * 16));
+            // pairs past nc: an offset beyond the resource (the load returns zero, no branch --
+            // a branch around the load made the compiler wait for every load at its join)
+            const uint32_t off = (p < P0 || 2 * p < nc) ? toff + (uint32_t)p * (TPB * 16) : 0x80000000u;
+            const d2_t x = bld2(basis, off);
             v[2 * p] = x.x;
             v[2 * p + 1] = (p < P0 || 2 * p + 1 < nc) ? x.y : 0.0;
             if (p >= P0) last = 2 * p == nc - 1 ? x.x : (2 * p + 1 == nc - 1 ? x.y : last);
@@ -728,7 +753,9 @@ template <int MAXC, int FMT>
 #endif
 #if TK_D1_OCCT
 // narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
-#if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
+#if TK_D1_OCCT == 3   // with even-column rows from E (fewer registers per pair)
+#define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 24 ? 6 : (MAXC <= 32 ? 5 : (MAXC <= 48 ? 4 : 3))))
+#elif TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
 #define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 16 ? 6 : (MAXC <= 24 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3))))
 #else
 #define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
@@ -818,10 +845,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         const bool ok = r >= 0 && r < a.n;
         const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * 16) : 0x80000000u;
         Row<MAXC> R;
-        int jl = j;   // the per-pair conditions are re-derived each window (hoisted: SGPR spills)
+        // odd j: column j-1 was written to E by the previous step (the pair (j-1, j) is stored
+        // once, below), so the row loads the complete pairs of columns 0..j-2 and takes
+        // column j-1 from E
+        int jl = j & ~1;   // the per-pair conditions are re-derived each window (hoisted: SGPR spills)
         asm volatile("" : "+s"(jl));
-        R.loadm(tv, toff, jl);
+        R.loadm_even(tv, toff, jl);
+        // (both loads issued before the patch below waits for the row)
         const double up = inb ? ld(Uin, r) : 0.0;
+        const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
+        if (j & 1) R.set_col(j - 1, e);
         // the step's scalars, evaluated by the last block of the previous step's reduce
         // (k_reduce256): RED1 = [c (j) | q (j) | |u|^2, <u,z>, .. (3j+3 values) | ib, gamma, ..]
         const double* s1 = d.RED1 + (j > 0 ? 3 * j + 3 : 2);
@@ -856,7 +889,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         D1_PHASE(2);
         const bool own = ok && t >= 2 * hl && t < TPB - 2 * hu;
         if (own) {
-            st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, (j & 1) ? R.last : 0.0);
+            if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, R.last);   // (v_{j-1}, v_j)
+            else st(d.E, r, vj);
             st(Uout, r, u);
         }
         const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
@@ -1026,7 +1060,9 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     const bool ok = r < a.n;
     const double* Vt = d.V + (int64_t)slot * TS;
     const uint32_t toff = t * 16u;
-    const rsrc_t tv = mkrsrc(Vt, vrange(nc));
+    // one-sweep Arnoldi after an even step: column j is in E, its pair in V is not written yet
+    const bool em = MODE == 0 && a.ecol == j;
+    const rsrc_t tv = mkrsrc(Vt, vrange(em ? j : nc));
     const bool gram = d.track_gram != 0;
     double* acc = lds;
     const double inv_beta = ld(d.sc, SC_INVBETA);
@@ -1048,7 +1084,8 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
         return;
     }
     Row<MAXC> R;
-    R.load(tv, toff, nc);
+    R.load(tv, toff, em ? j : nc);
+    if (em) R.set_col(j, ok ? ld(d.E, r) : 0.0);
     double v;
     if (MODE == 0) {
         const double up = ld(a.ubuf ? d.W : d.U, r);
