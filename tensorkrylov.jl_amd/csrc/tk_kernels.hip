@@ -753,9 +753,7 @@ template <int MAXC, int FMT>
 #endif
 #if TK_D1_OCCT
 // narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
-#if TK_D1_OCCT == 3   // with even-column rows from E (fewer registers per pair)
-#define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 24 ? 6 : (MAXC <= 32 ? 5 : (MAXC <= 48 ? 4 : 3))))
-#elif TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
+#if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
 #define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 16 ? 6 : (MAXC <= 24 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3))))
 #else
 #define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
