@@ -179,7 +179,8 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
 /* basis_tensor_mul! (src/utils.jl:478-488, called at src/tensor_krylov_method.jl:112):
  * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).
  * Y: host [nf][t][k] (each Y_s column-major k x t).  X: host [nf][t][n] (column-major
- * n x t each) or NULL to leave the product on the device (benchmarks).
+ * n x t each) or NULL to leave the product on the device (benchmarks; on the device X_s
+ * is tile-major like V_s: 256-row tiles, each tile's t columns of 256 rows contiguous).
  * A pending column is finalized first (as tk_decomp_flush, its record in the flush slot);
  * for TK_ARNOLDI with k <= the step count <= 64, in the same launch as the product: the
  * flush's register row of each basis tile also forms the product (FP64 FMAs, Y through the

@@ -1426,11 +1426,18 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
         RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");
     }
     if (X) {
+        // device X_s is tile-major (256-row tiles, each tile's t columns contiguous): copy
+        // and reorder to column-major n x t
         HIPCHK(hipStreamSynchronize(s));
-        for (int f = 0; f < dc->nf; ++f)
-            HIPCHK(hipMemcpy2D(X + (size_t)f * dc->n * t, dc->n * sizeof(double),
-                               dc->Xdev + (size_t)f * dc->ld * t, dc->ld * sizeof(double),
-                               dc->n * sizeof(double), t, hipMemcpyDeviceToHost));
+        std::vector<double> tmp((size_t)dc->ld * t);
+        for (int f = 0; f < dc->nf; ++f) {
+            HIPCHK(hipMemcpy(tmp.data(), dc->Xdev + (size_t)f * dc->ld * t, tmp.size() * sizeof(double),
+                             hipMemcpyDeviceToHost));
+            double* Xf = X + (size_t)f * dc->n * t;
+            for (int q = 0; q < t; ++q)
+                for (int64_t r = 0; r < dc->n; ++r)
+                    Xf[(size_t)q * dc->n + r] = tmp[(size_t)(r >> 8) * 256 * t + (size_t)q * 256 + (r & 255)];
+        }
     }
     return TK_OK;
     TK_API_END

@@ -329,16 +329,17 @@ __device__ __forceinline__ void row_dot2(const Row<MAXC>& R, const double* __res
     sh = a0 + a1;
     sg = b0 + b1;
 }
-// Same with both coefficient vectors staged in LDS (broadcast ds_read_b128), same order.
-template <int MAXC>
+// Same with both coefficient vectors staged in LDS (broadcast ds_read_b128), same order;
+// coefficient reads in groups of GRP columns (register pressure).
+template <int MAXC, int GRP = 8>
 __device__ __forceinline__ void row_dot2_lds(const Row<MAXC>& R, const double* __restrict__ h,
                                              const double* __restrict__ g, double& sh, double& sg) {
     double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
 #pragma unroll
-    for (int c0 = 0; c0 < MAXC; c0 += 8) {
-        __builtin_amdgcn_sched_barrier(0);   // coefficient reads in groups of 8 (register pressure)
+    for (int c0 = 0; c0 < MAXC; c0 += GRP) {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int c = c0; c < c0 + 8; c += 2) {
+        for (int c = c0; c < c0 + GRP; c += 2) {
             const d2_t hv = *(const d2_t*)(h + c);
             const d2_t gv = *(const d2_t*)(g + c);
             a0 += R.v[c] * hv.x;
@@ -684,6 +685,17 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 
 #ifndef TK_BK_TEST
 #define TK_BK_TEST 0
+#endif
+#ifndef TK_VY_TEST
+#define TK_VY_TEST 0
+#endif
+// fused flush + V*Y (k_fin_vy): 4 waves per SIMD up to this register-row width (56 spills to
+// scratch at 4), Y coefficient reads from LDS in groups of this many columns
+#ifndef TK_VY_OCC4
+#define TK_VY_OCC4 48
+#endif
+#ifndef TK_VY_GRP
+#define TK_VY_GRP 8
 #endif
 // occupancy by register-row width (measured at C2: 4 waves/SIMD up to 32 columns, 3 up
 // to 56; 40 columns at 4 waves spill)
@@ -1081,6 +1093,9 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
         }
         return;
     }
+    double* Ys = lds + (NG + 1) * TPB;   // VY: Y_s staged in LDS (tq x ldy)
+    if constexpr (VY)
+        for (int i = t; i < tq * ldy; i += TPB) Ys[i] = ld(Yf, i);
     Row<MAXC> R;
     R.load(tv, toff, em ? j : nc);
     if (em) R.set_col(j, ok ? ld(d.E, r) : 0.0);
@@ -1096,13 +1111,24 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     if constexpr (VY) {
         // X_s[r, q] = sum_{c < k} V[r, c] Y_s[c, q] from the register row the flush just
         // loaded (the tile is streamed once for both); Y_s columns zero-padded to ldy >= MAXC
-        // (so columns k..j of the row meet zeros), read through the scalar cache two at a time
+        // (so columns k..j of the row meet zeros), two columns at a time from LDS (broadcast
+        // reads; through the scalar cache each group of coefficients was a dependent round trip)
+        __syncthreads();
         for (int q = 0; q < tq; q += 2) {
             double x0, x1;
+#if TK_VY_TEST & 2   // (timing experiment: no products)
+            x0 = R.v[q & 7]; x1 = R.v[(q + 1) & 7];
+#elif TK_VY_TEST & 4   // (the scalar-cache form)
             row_dot2<MAXC>(R, Yf + (int64_t)q * ldy, Yf + (int64_t)(q + 1 < tq ? q + 1 : q) * ldy, x0, x1);
-            if (ok) {
-                st(Xf, r + (int64_t)q * a.ld, x0);
-                if (q + 1 < tq) st(Xf, r + (int64_t)(q + 1) * a.ld, x1);
+#else
+            row_dot2_lds<MAXC, TK_VY_GRP>(R, Ys + q * ldy, Ys + (q + 1 < tq ? q + 1 : q) * ldy, x0, x1);
+#endif
+            // X tile-major like V: the tile's tq columns of 256 rows are one contiguous block,
+            // so the stores stream (column-major n x t stores cost a third of the kernel)
+            if (ok && !(TK_VY_TEST & 1)) {
+                double* Xt = Xf + (int64_t)slot * TPB * tq + t;
+                st(Xt, (int64_t)q * TPB, x0);
+                if (q + 1 < tq) st(Xt, (int64_t)(q + 1) * TPB, x1);
             }
         }
     }
@@ -1858,7 +1884,8 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
         __syncthreads();
         if (r < a.n) {
             const int cn = min(16, tn - 16 * q);
-            for (int c = 0; c < cn; ++c) st(X, r + (int64_t)(t0 + 16 * q + c) * a.ld, Xs[c * XS_STRIDE + threadIdx.x]);
+            for (int c = 0; c < cn; ++c)   // X tile-major (as k_fin_vy)
+                st(X, (int64_t)tile * TPB * t + (int64_t)(t0 + 16 * q + c) * TPB + threadIdx.x, Xs[c * XS_STRIDE + threadIdx.x]);
         }
     }
 }
@@ -1877,7 +1904,7 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
 // block: the register row the flush loads also feeds the product, so each basis tile is
 // streamed from HBM once for both.  Y: [nf][t][ldy] with zero rows k..ldy-1, k <= j + 1.
 template <int MAXC>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= 32 ? 4 : 3, MAXC <= 32 ? 4 : 3)))
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= TK_VY_OCC4 ? 4 : 3, MAXC <= TK_VY_OCC4 ? 4 : 3)))
 void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Yall, double* __restrict__ Xall,
               int ldy, int t) {
     extern __shared__ __attribute__((aligned(16))) double lds[];   // acc[NG + 1][256]
@@ -2039,7 +2066,7 @@ void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s
 void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s) {
     const int nc = a.j + 1;
     const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
-    const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
+    const size_t lds = ((size_t)((M + 15) / 16 + 1) * TPB + (size_t)t * ldy) * sizeof(double);   // acc + Y_s
     const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
     with_maxc(nc, [&](auto Mc) {
         hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
