@@ -65,6 +65,10 @@ def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None):
         return 8 * n * (k - 1) + 3 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
     if method == "TensorArnoldi":
         return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
+    if method == "TensorLanczos" and sweeps == 1:
+        # one-sweep TTR (k_lan_1s): u_{k-1} and v_{k-1} read, v_k and u_k written, <v_k, b>;
+        # the SpMV takes v_k from LDS (+ the tracked factor's Gram row, gram_bytes_step)
+        return 5 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
     b = b_spmv + 8 * n + 8 * n + 8 * n
     if method == "TensorLanczosReorth":
         b += 8 * n * (k + 1)
@@ -145,7 +149,7 @@ def main():
         t_rank = 17 if sym else 3
     rng = np.random.default_rng(7)
     Ys = [rng.standard_normal((K, t_rank)) for _ in range(part.nf)]
-    sweeps = dev.arnoldi_sweeps if method == "TensorArnoldi" else 0
+    sweeps = dev.arnoldi_sweeps if method in ("TensorArnoldi", "TensorLanczos") else 0
 
     host_issue = [0.0, 0]
 
@@ -266,6 +270,10 @@ def main():
     # roofline of the Arnoldi step (SpMV + MGS2 + reductions), device time from events
     alg_step = sum(alg_bytes_step(n, nnz, k, method, sweeps, toeplitz_bytes(csc))
                    for k in range(1, K + 1)) * part.nf
+    if method == "TensorLanczos" and sweeps == 1 and part.first == 0:
+        # the Gram row of factor 1's new column (orthogonality_loss, src/tensor_krylov_method.jl
+        # :103): its basis row is streamed for it alone
+        alg_step += sum(8 * n * (k - 1) for k in range(1, K + 1))
     step_avg_s = (step_ms / 1e3) / max(step_cnt, 1)
     achieved = (alg_step / K) / step_avg_s / 1e9 if step_cnt else None
     # the same steps priced in the reference algorithm's bytes (MGS2 streams V

@@ -120,8 +120,9 @@ tk_status tk_decomp_destroy(tk_decomp* dc);
 
 /* Sweeps over V per TK_ARNOLDI step: 1 = CGS2 with the reorthogonalization delayed by one
  * step (every local A_s banded, DIA with bandwidths <= 4), 2 = CGS2
- * (other storage, or TKHIP_ARNOLDI=cgs2 in the environment at create); 0 for the
- * Lanczos methods. */
+ * (other storage, or TKHIP_ARNOLDI=cgs2 in the environment at create).  TK_LANCZOS: 1 for
+ * the one-sweep TTR (banded A_s; TKHIP_LANCZOS=ttr keeps the three-pass kernels: 0);
+ * TK_LANCZOS_REORTH: 0. */
 int tk_decomp_arnoldi_sweeps(tk_decomp* dc);
 
 /* 1 when the records exchange of this handle is triggered by a signal word the step's last

@@ -671,9 +671,14 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     // Arnoldi runs as one sweep per step (k_arn_d1) when every local factor is banded
     // (DIA, bandwidths <= 4: the SpMVs read their vector from the window in LDS) and its
     // basis is addressable with 31-bit offsets; TKHIP_ARNOLDI=cgs2 keeps the two-sweep CGS2.
+    // TensorLanczos likewise (k_lan_1s: TTR with the orthogonalization against v_j delayed a
+    // step); TKHIP_LANCZOS=ttr keeps the three-pass TTR kernels.
     {
         const char* e = getenv("TKHIP_ARNOLDI");
-        bool ok = method == TK_ARNOLDI && !(e && strcmp(e, "cgs2") == 0) && (dc->fmt == 1 || dc->fmt == 5);
+        const char* el = getenv("TKHIP_LANCZOS");
+        bool ok = ((method == TK_ARNOLDI && !(e && strcmp(e, "cgs2") == 0)) ||
+                   (method == TK_LANCZOS && !(el && strcmp(el, "ttr") == 0))) &&
+                  (dc->fmt == 1 || dc->fmt == 5);
         const double vbytes = (double)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double);
         ok = ok && vbytes < 2147483648.0 - 1048576.0;
         for (int f = 0; ok && f < nf; ++f) ok = mats[f]->hl <= 4 && mats[f]->hu <= 4;
@@ -836,7 +841,9 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
 int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
 
 int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
-    if (!dc || dc->method != TK_ARNOLDI) return 0;
+    if (!dc) return 0;
+    if (dc->method == TK_LANCZOS) return dc->onesweep ? 1 : 0;
+    if (dc->method != TK_ARNOLDI) return 0;
     return dc->onesweep ? 1 : 2;
 }
 
@@ -1054,7 +1061,13 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 3, j + 3, np, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_ARN_FIN, 0, 1, s), "post");
     } else {
-        if (fd) {
+        if (fd && dc->onesweep && j <= ARN_D1_JMAX) {
+            // one-sweep Lanczos: v_{j+1} = inv(beta) .* (u_j - alpha v_j) from the step's buffers
+            KArgs f = a;
+            f.ubuf = (j & 1) ? 0 : 1;
+            f.ecol = (j & 1) ? -1 : j;
+            RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, f, 2, s), "fin_d");
+        } else if (fd) {
             RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, a, 1, s), "fin_d");
         } else {
             RUN(TCLS_FIN, 2, launch_lan_finalize(dc->df, nf, a, s), "lan_finalize");
@@ -1083,7 +1096,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         ax.seq = ++dc->seq;
     }
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
-    if (dc->method == TK_ARNOLDI && dc->onesweep && j > ARN_D1_JMAX && dc->pending && dc->last_j <= ARN_D1_JMAX) {
+    if ((dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && j > ARN_D1_JMAX && dc->pending &&
+        dc->last_j <= ARN_D1_JMAX) {
         // leaving the one-sweep range: write the pending column v_j (its record is
         // overwritten by the CGS2 step below, which reports column j again)
         tk_status st2 = bk_flush(dc);
@@ -1124,6 +1138,13 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN, fused ? 1 : 0, 1, s), "post");
+        dc->pending = true;
+    } else if (dc->method == TK_LANCZOS && dc->onesweep && j <= ARN_D1_JMAX) {
+        // one sweep: writes v_j (E or its pair) and u_j; the reduce's last block takes
+        // alpha_j, beta_j and writes the step's record (no post launch)
+        a.ubuf = j & 1;
+        RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->npd, s), "lan_1s");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 4 + j, 0, s, 0, RED_LAN, &ax), "reduce");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;
@@ -1334,7 +1355,8 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     HIPCHK(hipSetDevice(dc->ctx->device));
     // (one-sweep Arnoldi after an even step: column last_j is still in DFac::E; the flush
     // stores it with the pending column)
-    const bool in_e = dc->method == TK_ARNOLDI && dc->onesweep && dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+                      dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     if (dc->pending && nc > 0 && c0 + nc - 1 >= dc->last_j + (in_e ? 0 : 1)) {
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;

@@ -15,6 +15,7 @@ enum {
     SC_INVB = 3,      // inv(norm(b))
     SC_BNORM = 4,     // norm(b)
     SC_REDO = 5,      // LanczosReorth: 1 when this step's loss check asks for the MGS redo
+    SC_ALPHA = 6,     // one-sweep Lanczos: alpha of the last step (its pending column's w = u - alpha v)
     SC_COUNT = 8
 };
 
@@ -102,6 +103,8 @@ constexpr int ARN_D1_JMAX = 63;
 // RED1 length: 3 kmax + 8 reduced values, plus the span one-sweep register rows read past
 // the live coefficients (2 x 64 + 16)
 #define RED1_LEN(kmax) (3 * (kmax) + 8 + 144)
+// launch_reduce's coefJ for a one-sweep Lanczos step (k_lan_1s)
+#define RED_LAN (-2)
 // where a one-sweep step's reduced dots (3j+6 values) are followed by the next step's
 // scalars (k_reduce256's last block): ib, gamma, beta, t1
 #define D1S_IB 0
@@ -126,6 +129,7 @@ void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s);   // j in 1..64
@@ -136,7 +140,7 @@ void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s);
 // npart <= 0: each factor's own DFac::npd partials (one-sweep Arnoldi)
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0,
-                   int coefJ = -1);
+                   int coefJ = -1, const KArgs* ax = nullptr);
 // post-processing (one 64-thread block per factor)
 enum PostKind {
     POST_INIT_A = 0,

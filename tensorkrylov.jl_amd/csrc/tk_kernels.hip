@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -95,6 +96,10 @@ __device__ __forceinline__ double mul_rn(double a, double b) {
 __device__ __forceinline__ double add_rn(double a, double b) {
 #pragma clang fp contract(off)
     return a + b;
+}
+__device__ __forceinline__ double sub_rn_(double a, double b) {
+#pragma clang fp contract(off)
+    return a - b;
 }
 
 // DPP row rotate (16-lane rows) of a double.
@@ -1020,6 +1025,99 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
 }
 
+// ------------------------------------------------------------------ Lanczos, one sweep per step
+// TTR (src/orthogonal_bases.jl:39-67) with the orthogonalization against v_j delayed into the
+// next step: step j enters with u_{j-1} = A v_{j-1} - beta_{j-2} v_{j-2} (U or W) and the
+// previous reduce's alpha_{j-1}, inv(beta_{j-1}), beta_{j-1} (DFac::sc), and per row
+//   w   = u_{j-1} - alpha_{j-1} v_{j-1}              (:53)
+//   v_j = inv(beta_{j-1}) .* w                        (:59; zero when beta == 0)   -> E / V
+//   u_j = A v_j - beta_{j-1} v_{j-1}                  (:45-47)                     -> other buffer
+//   P1  = [ <u_j,v_j>, |u_j|^2, |v_j|^2, <v_j,b> | gram <V[:,c],v_j> (c<j, tracked factor) ]
+// The reduce's last block then takes alpha_j = <u_j,v_j> (:50) and
+// beta_j = ||u_j - alpha_j v_j|| = sqrt(|u|^2 - 2 alpha^2 + alpha^2 |v|^2) (:56) and writes the
+// step's record.  One banded SpMV from LDS (window halo as k_arn_d1); the basis row is loaded
+// only for the factor that tracks the Gram row.  Products and sums separately rounded like the
+// reference's broadcasts.  Columns written once (even j -> E, odd j -> the pair).
+template <int MAXC, int FMT>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_lan_1s(const DFac* __restrict__ F, KArgs a) {
+#pragma clang fp contract(off)
+    constexpr int NG = (MAXC + 15) / 16;
+    __shared__ double xv[TPB];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const DFac& d = F[blockIdx.y];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= d.nwin) return;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    double* acc = lds;   // [1 + NG chunks][64]: 4 wave slots per value
+    const int j = a.j, t = threadIdx.x;
+    const int hl = d.hl, hu = d.hu, WS = TPB - 2 * (hl + hu);
+    const double* Uin = a.ubuf ? d.W : d.U;
+    double* Uout = a.ubuf ? d.U : d.W;
+    const double alpha = ld(d.sc, SC_ALPHA), ib = ld(d.sc, SC_INVBETA), betap = ld(d.sc, SC_BETAPREV);
+    const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
+    const bool gram = d.track_gram != 0;
+    const int nch = 1 + (gram ? NG : 0);
+    for (int k = t; k < nch * 64; k += TPB) acc[k] = 0.0;
+    const int64_t S = (int64_t)slot * WS - 2 * hl;
+    const int64_t r = S + t;
+    const bool inb = r >= 0 && r < a.ld;
+    const bool ok = r >= 0 && r < a.n;
+    const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * 16) : 0x80000000u;
+    Row<MAXC> R;
+    int jl = j & ~1;
+    asm volatile("" : "+s"(jl));
+    if (gram) R.loadm_even(tv, toff, jl);
+    const double up = inb ? ld(Uin, r) : 0.0;
+    // v_{j-1}: E after an even step, the odd half of its pair otherwise
+    const double vp = j == 0 ? 0.0 : ((j & 1) ? (inb ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j - 1)));
+    const double bv = ok ? ld(d.b, r) : 0.0;
+    if (gram && (j & 1)) R.set_col(j - 1, vp);
+    const double w = sub_rn_(up, mul_rn(alpha, vp));
+    const double vj = ok ? mul_rn(ib, w) : 0.0;
+    xv[t] = vj;
+    __syncthreads();
+    const double av = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
+    const double u = ok ? sub_rn_(av, mul_rn(betap, vp)) : 0.0;
+    const bool own = ok && t >= 2 * hl && t < TPB - 2 * hu;
+    if (own) {
+        if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, vp);
+        else st(d.E, r, vj);
+        st(Uout, r, u);
+    }
+    const double uo = own ? u : 0.0, vo = own ? vj : 0.0;
+    {
+        double x[16] = {uo * vj, uo * u, vo * vj, vo * bv};
+        D1_ACC(0, x);
+    }
+    if (gram) {
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            if (16 * k < j) {
+                double x[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = R.v[16 * k + i < MAXC ? 16 * k + i : 0] * (16 * k + i < MAXC ? vo : 0.0);
+                D1_ACC(1 + k, x);
+            }
+        }
+    }
+    __syncthreads();
+    // combine the 4 wave slots of every value -> P1 [ 4 scalars | gram (c<j) ]
+    for (int e = t; e < nch * 16; e += TPB) {
+        const int k = e >> 4, sl = e & 15;
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < D1_NP; ++p) sum += D1_PART(k, p, sl);
+        int vi = -1;
+        if (k == 0) {
+            if (sl < 4) vi = sl;
+        } else {
+            const int col = 16 * (k - 1) + sl;
+            if (col < j) vi = 4 + col;
+        }
+        if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
+    }
+}
+
 // Initialization for the one-sweep Arnoldi: V[:,0] = U = inv(norm(b)) .* b
 // (src/decompositions.jl:112-118) and the first projection of A v_0 (v_0 is known at
 // every row from b, so the SpMV needs no halo):
@@ -1071,16 +1169,25 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     const double* Vt = d.V + (int64_t)slot * TS;
     const uint32_t toff = t * 16u;
     // one-sweep Arnoldi after an even step: column j is in E, its pair in V is not written yet
-    const bool em = MODE == 0 && a.ecol == j;
+    const bool em = (MODE == 0 || MODE == 2) && a.ecol == j;
     const rsrc_t tv = mkrsrc(Vt, vrange(em ? j : nc));
     const bool gram = d.track_gram != 0;
     double* acc = lds;
     const double inv_beta = ld(d.sc, SC_INVBETA);
-    if (MODE == 1 && !gram) {
+    // MODE 2 (one-sweep Lanczos): v = inv(beta) .* (u - alpha v_j), u = the last step's raw vector
+    const double alpha2 = MODE == 2 ? ld(d.sc, SC_ALPHA) : 0.0;
+    const double up2 = MODE == 2 ? ld(a.ubuf ? d.W : d.U, r) : 0.0;
+    if (MODE >= 1 && !gram) {
         // Lanczos without a Gram row: v, the pair store (other half = column j), <v,b>
-        const bool zero = ld(d.sc, SC_BETA) == 0.0;
-        const double v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
-        const double other = ((j + 1) & 1) ? bld(tv, toff + cofs(j)) : 0.0;
+        const double vjc = em ? (ok ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j));
+        double v;
+        if (MODE == 2) {
+            v = ok ? mul_rn(inv_beta, sub_rn_(up2, mul_rn(alpha2, vjc))) : 0.0;
+        } else {
+            const bool zero = ld(d.sc, SC_BETA) == 0.0;
+            v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
+        }
+        const double other = ((j + 1) & 1) ? vjc : 0.0;
         st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, other);
         double x[16] = {v * ld(d.b, r)};
         acc[t] = rs16(x);
@@ -1103,6 +1210,8 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     if (MODE == 0) {
         const double up = ld(a.ubuf ? d.W : d.U, r);
         v = ok ? (up - row_dot<MAXC, true>(R, tv, toff, nc, d.h2)) * inv_beta : 0.0;
+    } else if (MODE == 2) {
+        v = ok ? mul_rn(inv_beta, sub_rn_(up2, mul_rn(alpha2, R.last))) : 0.0;   // R.last = column j
     } else {
         const bool zero = ld(d.sc, SC_BETA) == 0.0;
         v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
@@ -1390,12 +1499,17 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 // Same for the one-sweep kernel's per-window partials (npart = DFac::npd, ~4k at n = 2^20):
 // four waves per value, each lane a strided subset in rounds of 16 independent loads, DPP
 // row sums, the 16 row totals summed in fixed order.
+__device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent);
+// coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
+// RED_LAN: one-sweep Lanczos step (nv = 4 + j; 4 for factors without a Gram row; the last
+// block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
 __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
-                                                   int coefJ) {
+                                                   int coefJ, KArgs ax) {
     __shared__ double rs[16];
     __shared__ int last;
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
+    if (coefJ == RED_LAN && !d.track_gram) nv = 4;
     if (c >= nv) return;
     const int npart = np > 0 ? np : d.npd;
     const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
@@ -1418,7 +1532,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         double r = 0.0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) r += rs[q];
-        if (coefJ < 0) {
+        if (coefJ < 0 && coefJ != RED_LAN) {
             st(which == 1 ? d.RED1 : d.RED2, c, r);
         } else {
             // one-sweep step: publish the value coherently (agent-scope store, through to the
@@ -1429,16 +1543,52 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
         }
     }
-    if (coefJ < 0) return;
+    if (coefJ < 0 && coefJ != RED_LAN) return;
     __syncthreads();
-    if (!last || t >= 64) return;
+    if (!last) return;
+    auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    if (coefJ == RED_LAN) {
+        // alpha_j = <u,v_j> (src/orthogonal_bases.jl:50), beta_j = ||u - alpha v_j|| (:56) from
+        // the dots (every thread alike), v_{j+1}'s scalars for the next step / the flush, and
+        // the step's record row (as POST_LAN: H[j,j], H[j+1,j], btilde_j = <v_j,b>, the Gram
+        // row of v_j) written through, with its host mirror, then the exchange / host signal
+        const int j = ax.j, kmax = ax.kmax;
+        const double al = cld(0), uu = cld(1), vv = cld(2), bt = cld(3);
+        const double bsq = add_rn(sub_rn_(uu, mul_rn(2.0 * al, al)), mul_rn(mul_rn(al, al), vv));
+        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+        const double ib = beta == 0.0 ? 0.0 : 1.0 / beta;
+        if (t == 0) {
+            st(d.sc, SC_ALPHA, al);
+            st(d.sc, SC_INVBETA, ib);
+            st(d.sc, SC_BETA, beta);
+            st(d.sc, SC_BETAPREV, beta);
+            __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        double* rec = ax.rec + (int64_t)d.gidx * ax.m;
+        double* hr = ax.hdone ? ax.hrec + (int64_t)d.gidx * ax.m : nullptr;
+        const int g0 = rec_gram(kmax);
+        for (int i = t; i < ax.m; i += 256) {
+            double v = 0.0;
+            if (i == j) v = al;
+            else if (i == j + 1) v = beta;
+            else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? cld(4 + i - g0) : vv) : 0.0;
+            else if (i == rec_beta(kmax)) v = beta;
+            else if (i == rec_bt(kmax)) v = bt;
+            else if (i == rec_col(kmax)) v = (double)j;
+            else if (i == rec_tracked(kmax)) v = d.track_gram ? 1.0 : 0.0;
+            __hip_atomic_store(rec + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (hr) __hip_atomic_store(hr + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        post_signal(ax, d, (int)blockIdx.y, true, true);
+        return;
+    }
+    if (t >= 64) return;
     // the next step's scalars from this step's dots (RED1 = c [0,J) | q [J,2J) | |u|^2 |
     // <u,z> ..., J = coefJ <= 65): beta = sqrt(|u|^2 - |c|^2), ib = inv(beta),
     // t1 = (<u,z> - c.q) ib, gamma = t1 ib = <v_J, A v_J> + (Hbar c)_J ib (the coefficient of
     // v_J in u_{J+1}).  One wave, coherent loads, a fixed-order butterfly; k_arn_d1's blocks
     // and the step's bookkeeping (bk_arn_d) read the results.
     const int J = coefJ;
-    auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     const double c0 = t < J ? cld(t) : 0.0, q0 = t < J ? cld(J + t) : 0.0;
     const double c1 = t + 64 < J ? cld(t + 64) : 0.0, q1 = t + 64 < J ? cld(J + 64 + t) : 0.0;
     const double uu = cld(2 * J), uz = cld(2 * J + 1);
@@ -1734,6 +1884,8 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
                 const double vav = ld(d.RED1, 2);
                 st(d.g, 0, vav);
                 st(d.sc, SC_INVBETA, 1.0);
+                st(d.sc, SC_ALPHA, 0.0);      // (one-sweep Lanczos step 0: v_0 = 1 .* (U - 0 * 0),
+                st(d.sc, SC_BETAPREV, 0.0);   //  u_0 = A v_0 - 0 * 0)
                 double* o = d.RED1 + 2;   // (k_arn_d1 step 0 reads its scalars here)
                 st(o, D1S_IB, 1.0);
                 st(o, D1S_GAMMA, vav);
@@ -2014,6 +2166,16 @@ void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t 
         hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
     });
 }
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+    const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
+    const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
+    with_band_fmt(a.fmt, [&](auto FM) {
+        with_maxc(a.j, [&](auto M) {
+            hipLaunchKernelGGL((k_lan_1s<decltype(M)::value, decltype(FM)::value>), dim3((npd + 7) / 8 * 8, nf),
+                               dim3(TPB), lds, s, F, a);
+        });
+    });
+}
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
@@ -2060,7 +2222,8 @@ void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s
     const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
     with_maxc(nc, [&](auto Mc) {
         if (mode == 0) hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 0>), grid, dim3(TPB), lds, s, F, a);
-        else hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 1>), grid, dim3(TPB), lds, s, F, a);
+        else if (mode == 1) hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 1>), grid, dim3(TPB), lds, s, F, a);
+        else hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 2>), grid, dim3(TPB), lds, s, F, a);
     });
 }
 void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s) {
@@ -2075,11 +2238,14 @@ void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, doubl
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
-void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ) {
+void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ,
+                   const KArgs* ax) {
+    KArgs none;
+    memset(&none, 0, sizeof(none));
     if (npart <= 0 && !gate)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ);
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
     else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1);
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1, none);
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }

@@ -128,7 +128,8 @@ class DeviceDecomposition:
     @property
     def arnoldi_sweeps(self):
         """Sweeps over V per Arnoldi step (1: delayed-reorthogonalization CGS2 on banded
-        A_s, 2: CGS2), 0 for the Lanczos methods (tk_decomp_arnoldi_sweeps)."""
+        A_s, 2: CGS2); TensorLanczos 1 for the one-sweep TTR on banded A_s, else 0;
+        LanczosReorth 0 (tk_decomp_arnoldi_sweeps)."""
         return int(self.ctx._lib.tk_decomp_arnoldi_sweeps(self.h))
 
     @property

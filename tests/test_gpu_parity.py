@@ -222,9 +222,16 @@ def test_arnoldi_mid_run_flush(ctx, cls):
         assert np.array_equal(x, y) if exact else np.abs(x - y).max() <= 1e-12
 
 
+@pytest.mark.parametrize("ttr", ["auto", "ttr"])
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20),
                                      ("Laplace", 700, 75)])
-def test_lanczos_matches_oracle(ctx, cls, n, K):
+def test_lanczos_matches_oracle(ctx, cls, n, K, ttr, monkeypatch):
+    """'auto': banded A_s take the one-sweep Lanczos (k_lan_1s; beyond step 63 the TTR
+    kernels), 'ttr': TKHIP_LANCZOS=ttr forces the three-pass TTR kernels."""
+    if ttr == "ttr":
+        monkeypatch.setenv("TKHIP_LANCZOS", "ttr")
+    else:
+        monkeypatch.delenv("TKHIP_LANCZOS", raising=False)
     tk = _tk()
     csc = tk.assemble_matrix(n, cls)
     bs = _rhs(n, 2, 11, distinct=True)
@@ -342,6 +349,22 @@ def test_basis_mul_mfma(ctx):
             assert np.abs(X[f] - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
     dev.close()
     A.close()
+
+
+def test_lanczos_mid_run_flush(ctx):
+    """One-sweep Lanczos: reading the basis mid-run flushes the pending column (after an even
+    step its predecessor is still in the column buffer); the run then continues and every
+    record and the final basis are bitwise those of the uninterrupted run."""
+    tk = _tk()
+    csc = tk.assemble_matrix(1500, "Laplace")
+    bs = _rhs(1500, 2, 23, distinct=True)
+    ra, Va = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20)
+    for peek in (8, 11):
+        rb, Vb = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20, peek=peek)
+        for x, y in zip(ra[:-1], rb[:-1]):
+            assert np.array_equal(x, y)
+        for x, y in zip(Va, Vb):
+            assert np.array_equal(x, y)
 
 
 @pytest.mark.parametrize("n,K", [(3000, 30), (1000, 70)])
