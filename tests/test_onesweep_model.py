@@ -65,3 +65,38 @@ def test_onesweep_model_matches_mgs2(cls, n, K):
     assert np.abs(H[:K + 1, :K] - ref.H[:K + 1, :K]).max() <= 1e-12 * scale
     assert np.abs(V - ref.V[:, :K + 1]).max() <= 1e-12
     assert np.abs(V.T @ V - np.eye(K + 1)).max() <= 1e-13
+
+
+def onesweep_lanczos(A, b, K):
+    """k_lan_1s + k_reduce256 (RED_LAN): TTR (src/orthogonal_bases.jl:39-67) with the
+    orthogonalization against v_j delayed into the next step; beta from the dots."""
+    n = len(b)
+    V = np.zeros((n, K + 1))
+    alpha_, beta_ = np.zeros(K), np.zeros(K)
+    U = (1.0 / np.linalg.norm(b)) * b                    # k_init_bd: U = v_0
+    alpha, ib, betap, vprev = 0.0, 1.0, 0.0, np.zeros(n)  # POST_INIT_B
+    for j in range(K):
+        vj = ib * (U - alpha * vprev)                    # :53, :59
+        V[:, j] = vj
+        u = A @ vj - betap * vprev                       # :45-47
+        a, uu, vv = u @ vj, u @ u, vj @ vj               # :50
+        beta = np.sqrt(max((uu - (2.0 * a) * a) + (a * a) * vv, 0.0))   # :56
+        alpha_[j], beta_[j] = a, beta
+        alpha, ib, betap, vprev, U = a, (0.0 if beta == 0.0 else 1.0 / beta), beta, vj, u
+    V[:, K] = ib * (U - alpha * vprev)                   # the flush (k_fin_d MODE 2)
+    return V, alpha_, beta_
+
+
+@pytest.mark.parametrize("n,K", [(200, 50), (200, 150), (3000, 60), (10000, 120)])
+def test_onesweep_lanczos_model_matches_ttr(n, K):
+    D = O.laplace_dense(n)
+    b = np.random.default_rng(n + K).random(n)
+    b /= np.linalg.norm(b)
+    ref = O.lanczos_algorithm(O.dense_to_csc(D), b, K + 1)     # K TTR steps
+    V, al, be = onesweep_lanczos(sp.csr_matrix(D), b, K)
+    ra = np.array([ref.H[i, i] for i in range(K)])
+    rb = np.array([ref.H[i + 1, i] for i in range(K)])
+    scale = max(np.abs(ra).max(), np.abs(rb).max())
+    assert np.abs(al - ra).max() <= 1e-13 * scale
+    assert np.abs(be - rb).max() <= 1e-13 * scale
+    assert np.abs(V - ref.V[:, :K + 1]).max() <= 1e-12
