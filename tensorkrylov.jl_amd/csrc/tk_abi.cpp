@@ -566,6 +566,8 @@ struct tk_decomp {
     // step's KArgs), or bk_flush launches it on its own
     int bk_j = -1;
     KArgs bk_args;
+    bool mfspmv = false;    // CGS2 factors sharing one A_s: one gather per nonzero for all (k_spmv_mf)
+    double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
     // exchange stream waits (hipStreamWaitValue64) for xcount
@@ -693,6 +695,14 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     dc->hf.resize(nf);
     const int KP = kmax + 2, KC = kmax + 1;
     tk_status st = TK_OK;
+    {
+        // CGS2 over factors that share one gather-format A_s (TKHIP_MFSPMV=0 turns it off)
+        const char* e = getenv("TKHIP_MFSPMV");
+        bool ok = method == TK_ARNOLDI && !dc->onesweep && nf >= 2 && nf <= 8 && (dc->fmt == 2 || dc->fmt == 3) &&
+                  !(e && e[0] == '0');
+        for (int f = 1; ok && f < nf; ++f) ok = mats[f] == mats[0];
+        dc->mfspmv = ok;
+    }
 #define DA(ptr, bytes)                                          \
     do {                                                        \
         void* p_ = nullptr;                                     \
@@ -738,6 +748,15 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
         d.gidx = gi;
+        d.Uint = nullptr;
+        d.AU = nullptr;
+        d.ifs = f;
+        d.inf = nf;
+        if (dc->mfspmv) {
+            if (f == 0) DA(dc->Uint, (size_t)dc->ld * nf * sizeof(double));
+            d.Uint = dc->Uint;
+            DA(d.AU, (size_t)dc->ld * sizeof(double));
+        }
     }
     DA(dc->df, nf * sizeof(DFac));
     {
@@ -895,6 +914,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.hdone = nullptr;
     a.seq = 0;
     a.ecol = -1;
+    a.mfs = 0;
     return a;
 }
 
@@ -1130,6 +1150,11 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
         if (fused) {
+            if (dc->mfspmv) {
+                // A U of every factor from one gather per nonzero (bitwise the per-factor SpMV)
+                RUN(TCLS_PASS1, 2, launch_spmv_mf(dc->df, nf, a, s), "spmv_mf");
+                a.mfs = 1;
+            }
             RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");
         } else {
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");

@@ -68,6 +68,12 @@ struct DFac {
     // one-sweep Arnoldi: the even column written by the last even step (v_j, n rows); the
     // odd step after it stores the pair (v_{j-1}, v_j) once, so no column is written twice
     double* E;
+    // CGS2 with one A_s shared by all local factors: their raw vectors U interleaved
+    // (Uint[r * inf + ifs], shared by the group) feed one gather per nonzero for all factors
+    // (k_spmv_mf), whose A U lands in AU; null otherwise
+    double* Uint;
+    double* AU;
+    int ifs, inf;
     // one-sweep reduce: arrival counter of the step's value blocks (the last one evaluates
     // the next step's scalars, k_reduce256)
     unsigned int* ctr;
@@ -92,6 +98,7 @@ struct KArgs {
     unsigned long long* hdone;   // ... then stores `seq` to hdone[local factor] (host-mapped)
     unsigned long long seq;
     int ecol;         // flush of the one-sweep pending column: this column (j) is in DFac::E, not V (-1: none)
+    int mfs;          // CGS2 pass 1: A U comes from DFac::AU (k_spmv_mf ran), not from its own gathers
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
@@ -130,6 +137,7 @@ void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
 void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
+void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s);   // j in 1..64

@@ -546,6 +546,60 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
     store_partials(acc, d.P1, a.npart, 2);
 }
 
+// ------------------------------------------------------------------ one A_s, many factors
+// The CGS2 first pass of factors sharing one A_s (the C3 gallery: five factors, one random
+// sparse matrix) is bound by its random gathers of U: ~15 distinct cache lines per row per
+// factor move from L2 to L1 for 8 useful bytes each.  Interleaving the factors' U rows
+// (Uint[r][f], k_ilv) lets one gather per nonzero fetch the entries of every factor, and
+// k_spmv_mf writes each factor's A U with the same products and sums in the same order as its
+// own SpMV would (bitwise the same), which pass 1 then reads as one more streamed vector.
+// F[0] carries the group's Uint (all factors' descriptors point to it).
+__global__ __launch_bounds__(TPB) void k_ilv(const DFac* __restrict__ F, int nf, int64_t ld_) {
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r >= ld_) return;
+    double* Ui = F[0].Uint;
+    for (int f = 0; f < nf; ++f) st(Ui, r * nf + f, ld(F[f].U, r));
+}
+template <int FMT, int NFM>
+__global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int nf, KArgs a) {
+#pragma clang fp contract(off)
+    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    if (r >= a.ld) return;
+    const DFac& d0 = F[0];
+    const double* Ui = d0.Uint;
+    double s[NFM];
+#pragma unroll
+    for (int f = 0; f < NFM; ++f) s[f] = 0.0;
+    if (r < a.n) {
+        // the per-row order of spmv<FMT> (ascending column, products and sums rounded apart)
+        auto acc1 = [&](double v, int64_t c) {
+            double u[NFM];
+#pragma unroll
+            for (int f = 0; f < NFM; ++f) u[f] = f < nf ? ld(Ui, c * nf + f) : 0.0;
+#pragma unroll
+            for (int f = 0; f < NFM; ++f) s[f] = add_rn(s[f], mul_rn(v, u[f]));
+        };
+        const SpM& A = d0.A;
+        if (FMT == SPM_SELL) {
+            const int64_t t = r >> 8;
+            const int l = (int)(r & 255);
+            const int64_t base = GP(const long long, A.sptr)[t];
+            const int w = GP(const int, A.swidth)[t];
+            const int len = GP(const int, A.rowlen)[r];
+            for (int q = 0; q < w; ++q) {
+                const int64_t e = base + (int64_t)q * TPB + l;
+                if (q < len) acc1(ld(A.sval, e), (int64_t)GP(const int, A.scol)[e]);
+            }
+        } else {
+            const int p0 = GP(const int, A.rowptr)[r], p1 = GP(const int, A.rowptr)[r + 1];
+            for (int p = p0; p < p1; ++p) acc1(ld(A.val, p), (int64_t)GP(const int, A.col)[p]);
+        }
+    }
+#pragma unroll
+    for (int f = 0; f < NFM; ++f)
+        if (f < nf) st(F[f].AU, r, s[f]);
+}
+
 // ------------------------------------------------------------------ Arnoldi (CGS2)
 
 // First pass, v_j stored:  W = A v_j;  P1 = [ <V[:,c], W>, c = 0..j ].
@@ -593,7 +647,7 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
         Row<MAXC> R;
         R.load(tv, toff, j);
         const double* Ug = d.U;
-        const double au = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
+        const double au = !ok ? 0.0 : (a.mfs ? ld(d.AU, r) : spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }));
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double w = ok ? (au - row_dot<MAXC, SC>(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
@@ -2133,6 +2187,16 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
                                dim3(TPB), lds, s, F, a);
         });
     });
+}
+void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    const int nb = (int)((a.ld + TPB - 1) / TPB);
+    hipLaunchKernelGGL(k_ilv, dim3(nb), dim3(TPB), 0, s, F, nf, a.ld);
+    auto go = [&](auto FM) {
+        if (nf <= 4) hipLaunchKernelGGL((k_spmv_mf<decltype(FM)::value, 4>), dim3(nb), dim3(TPB), 0, s, F, nf, a);
+        else hipLaunchKernelGGL((k_spmv_mf<decltype(FM)::value, 8>), dim3(nb), dim3(TPB), 0, s, F, nf, a);
+    };
+    if (a.fmt == SPM_SELL) go(IC<SPM_SELL>{});
+    else go(IC<SPM_CSR>{});
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     const size_t lds = lds_bytes(a.j + 1, a.kmax, TK_A1_SCALAR ? 0 : 2);

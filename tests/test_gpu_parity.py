@@ -444,3 +444,24 @@ def test_fused_flush_basis_mul_identical(ctx, cls, n, t, monkeypatch):
         ref = Va[f][:, :K] @ Ys[f]
         for X in (Xa, Xb):
             assert np.abs(X[f] - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("nf,csr", [(5, False), (3, True)])
+def test_shared_matrix_spmv_bitwise(ctx, nf, csr, monkeypatch):
+    """CGS2 factors that share one gather-format A_s take A U from one interleaved gather per
+    nonzero (k_ilv + k_spmv_mf): records and bases bitwise those of the per-factor SpMV
+    (TKHIP_MFSPMV=0), SELL-256 and CSR storage."""
+    tk = _tk()
+    n, K = 4000, 24
+    csc = tk.assemble_matrix(n, "RandSparseSPD")
+    bs = _rhs(n, nf, 31, distinct=True)
+    if csr:
+        monkeypatch.setenv("TKHIP_FORCE_CSR", "1")
+    monkeypatch.delenv("TKHIP_MFSPMV", raising=False)
+    ra, Va = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, sweeps=2)
+    monkeypatch.setenv("TKHIP_MFSPMV", "0")
+    rb, Vb = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, sweeps=2)
+    for x, y in zip(ra, rb):
+        assert np.array_equal(x, y)
+    for x, y in zip(Va, Vb):
+        assert np.array_equal(x, y)
