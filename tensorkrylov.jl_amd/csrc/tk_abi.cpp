@@ -753,7 +753,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.ifs = f;
         d.inf = nf;
         if (dc->mfspmv) {
-            if (f == 0) DA(dc->Uint, (size_t)dc->ld * nf * sizeof(double));
+            if (f == 0) DA(dc->Uint, (size_t)dc->ld * 8 * sizeof(double));   // rows padded (ilv_pitch <= 8)
             d.Uint = dc->Uint;
             DA(d.AU, (size_t)dc->ld * sizeof(double));
         }

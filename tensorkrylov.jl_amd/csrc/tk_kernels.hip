@@ -554,11 +554,16 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 // k_spmv_mf writes each factor's A U with the same products and sums in the same order as its
 // own SpMV would (bitwise the same), which pass 1 then reads as one more streamed vector.
 // F[0] carries the group's Uint (all factors' descriptors point to it).
+// Uint rows are padded to ilv_pitch(nf) doubles (a power of two: one aligned 16..64-byte
+// piece per gather, read as 16-byte loads)
+__host__ __device__ inline int ilv_pitch(int nf) { return nf <= 2 ? 2 : (nf <= 4 ? 4 : 8); }
 __global__ __launch_bounds__(TPB) void k_ilv(const DFac* __restrict__ F, int nf, int64_t ld_) {
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
     if (r >= ld_) return;
     double* Ui = F[0].Uint;
-    for (int f = 0; f < nf; ++f) st(Ui, r * nf + f, ld(F[f].U, r));
+    const int p = ilv_pitch(nf);
+    for (int f = 0; f < p; f += 2)   // 16-byte stores
+        GP(d2_t, Ui + r * p)[f >> 1] = (d2_t){f < nf ? ld(F[f].U, r) : 0.0, f + 1 < nf ? ld(F[f + 1].U, r) : 0.0};
 }
 template <int FMT, int NFM>
 __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int nf, KArgs a) {
@@ -567,6 +572,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
     if (r >= a.ld) return;
     const DFac& d0 = F[0];
     const double* Ui = d0.Uint;
+    constexpr int NP = NFM <= 2 ? 2 : (NFM <= 4 ? 4 : 8);   // = ilv_pitch(NFM)
     double s[NFM];
 #pragma unroll
     for (int f = 0; f < NFM; ++f) s[f] = 0.0;
@@ -575,7 +581,11 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
         auto acc1 = [&](double v, int64_t c) {
             double u[NFM];
 #pragma unroll
-            for (int f = 0; f < NFM; ++f) u[f] = f < nf ? ld(Ui, c * nf + f) : 0.0;
+            for (int f = 0; f < NFM; f += 2) {
+                const d2_t x = GP(const d2_t, Ui + c * NP)[f >> 1];
+                u[f] = x.x;
+                if (f + 1 < NFM) u[f + 1] = x.y;
+            }
 #pragma unroll
             for (int f = 0; f < NFM; ++f) s[f] = add_rn(s[f], mul_rn(v, u[f]));
         };
@@ -586,9 +596,33 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
             const int64_t base = GP(const long long, A.sptr)[t];
             const int w = GP(const int, A.swidth)[t];
             const int len = GP(const int, A.rowlen)[r];
-            for (int q = 0; q < w; ++q) {
-                const int64_t e = base + (int64_t)q * TPB + l;
-                if (q < len) acc1(ld(A.sval, e), (int64_t)GP(const int, A.scol)[e]);
+            // slots in groups of SG: their indices and values, then all their gathers, are in
+            // flight together before the products are summed in order
+            constexpr int SG = 4;
+            for (int q0 = 0; q0 < w; q0 += SG) {
+                int64_t cc[SG];
+                double vv[SG];
+#pragma unroll
+                for (int g = 0; g < SG; ++g) {
+                    const int64_t e = base + (int64_t)(q0 + g) * TPB + l;
+                    const bool in = q0 + g < len;
+                    cc[g] = in ? (int64_t)GP(const int, A.scol)[e] : -1;
+                    vv[g] = in ? ld(A.sval, e) : 0.0;
+                }
+                double u[SG][NFM];
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+#pragma unroll
+                    for (int f = 0; f < NFM; f += 2) {
+                        const d2_t x = cc[g] >= 0 ? GP(const d2_t, Ui + cc[g] * NP)[f >> 1] : (d2_t){0.0, 0.0};
+                        u[g][f] = x.x;
+                        if (f + 1 < NFM) u[g][f + 1] = x.y;
+                    }
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    if (cc[g] >= 0)
+#pragma unroll
+                        for (int f = 0; f < NFM; ++f) s[f] = add_rn(s[f], mul_rn(vv[g], u[g][f]));
             }
         } else {
             const int p0 = GP(const int, A.rowptr)[r], p1 = GP(const int, A.rowptr)[r + 1];
@@ -596,8 +630,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
         }
     }
 #pragma unroll
-    for (int f = 0; f < NFM; ++f)
-        if (f < nf) st(F[f].AU, r, s[f]);
+    for (int f = 0; f < NFM; ++f) st(F[f].AU, r, s[f]);
 }
 
 // ------------------------------------------------------------------ Arnoldi (CGS2)
@@ -2192,8 +2225,16 @@ void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     const int nb = (int)((a.ld + TPB - 1) / TPB);
     hipLaunchKernelGGL(k_ilv, dim3(nb), dim3(TPB), 0, s, F, nf, a.ld);
     auto go = [&](auto FM) {
-        if (nf <= 4) hipLaunchKernelGGL((k_spmv_mf<decltype(FM)::value, 4>), dim3(nb), dim3(TPB), 0, s, F, nf, a);
-        else hipLaunchKernelGGL((k_spmv_mf<decltype(FM)::value, 8>), dim3(nb), dim3(TPB), 0, s, F, nf, a);
+        constexpr int FMv = decltype(FM)::value;
+        switch (nf) {   // the group size is a template parameter (2..8 factors)
+            case 2: hipLaunchKernelGGL((k_spmv_mf<FMv, 2>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            case 3: hipLaunchKernelGGL((k_spmv_mf<FMv, 3>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            case 4: hipLaunchKernelGGL((k_spmv_mf<FMv, 4>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            case 5: hipLaunchKernelGGL((k_spmv_mf<FMv, 5>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            case 6: hipLaunchKernelGGL((k_spmv_mf<FMv, 6>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            case 7: hipLaunchKernelGGL((k_spmv_mf<FMv, 7>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+            default: hipLaunchKernelGGL((k_spmv_mf<FMv, 8>), dim3(nb), dim3(TPB), 0, s, F, nf, a); break;
+        }
     };
     if (a.fmt == SPM_SELL) go(IC<SPM_SELL>{});
     else go(IC<SPM_CSR>{});
