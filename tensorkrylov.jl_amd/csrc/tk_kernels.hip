@@ -1596,7 +1596,9 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     __shared__ int last;
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
+    const int nvs = nv;   // (the scalars' place after the values)
     if (coefJ == RED_LAN && !d.track_gram) nv = 4;
+    if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
     const int npart = np > 0 ? np : d.npd;
     const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
@@ -1691,7 +1693,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
         const double ib = 1.0 / beta;
         const double t1 = (uz - cq) * ib;
-        double* o = d.RED1 + nv;
+        double* o = d.RED1 + nvs;
         st(o, D1S_IB, ib);
         st(o, D1S_GAMMA, t1 * ib);
         st(o, D1S_BETA, beta);
