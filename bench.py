@@ -135,7 +135,7 @@ def main():
     mcode = {"TensorArnoldi": L.TK_ARNOLDI, "TensorLanczos": L.TK_LANCZOS,
              "TensorLanczosReorth": L.TK_LANCZOS_REORTH}[method]
     dev = tkamd.DeviceDecomposition(ctx, mcode,
-                                    d, part.first, [A] * part.nf, bs, K)
+                                    d, part.first, [A] * part.nf, bs, K, n=n)
     # exp-sum rank at k = K (Laplace: kappa independent of n and d)
     sym = inst == "SymInstance"
     if sym and cls == "Laplace":

@@ -634,9 +634,11 @@ static void free_decomp(tk_decomp* dc) {
 tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,
                            tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
                            int track_all_gram, tk_decomp** out) { TK_API_BEGIN
-    CHECKARG(c && mats && b && out, "NULL argument");
+    CHECKARG(c && out && (nf == 0 || (mats && b)), "NULL argument");
     CHECKARG(method >= TK_ARNOLDI && method <= TK_LANCZOS_REORTH, "unknown method");
-    CHECKARG(nf >= 1 && d_total >= 1 && first_factor >= 0 && first_factor + nf <= d_total, "bad factor range");
+    // nf == 0: a rank of a job with more ranks than factors (it only takes part in the
+    // records all-reduce; every launch is skipped)
+    CHECKARG(nf >= 0 && d_total >= 1 && first_factor >= 0 && first_factor + nf <= d_total, "bad factor range");
     CHECKARG(kmax >= 1 && kmax <= 1000, "kmax out of range [1, 1000]");
     CHECKARG(n >= 1, "n must be positive");
     for (int f = 0; f < nf; ++f) {
@@ -666,7 +668,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     }
     {
         auto fmt_of = [](const tk_mat* A) { return A->ndiag > 0 ? (A->ndiag <= 4 ? (A->toep ? 5 : 1) : 4) : (A->sell ? 2 : 3); };
-        dc->fmt = fmt_of(mats[0]);
+        dc->fmt = nf > 0 ? fmt_of(mats[0]) : 0;
         for (int f = 1; f < nf; ++f)
             if (fmt_of(mats[f]) != dc->fmt) dc->fmt = 0;
     }

@@ -2209,12 +2209,15 @@ static void with_fmt(int fmt, F f) {
 }
 
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     hipLaunchKernelGGL(k_init_a, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     hipLaunchKernelGGL(k_init_b, dim3(a.npart, nf), dim3(TPB), lds_bytes(2, a.kmax, 0), s, F, a);
 }
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 1, a.kmax, 0);
     with_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j + 1, [&](auto M) {
@@ -2224,6 +2227,7 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     });
 }
 void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int nb = (int)((a.ld + TPB - 1) / TPB);
     hipLaunchKernelGGL(k_ilv, dim3(nb), dim3(TPB), 0, s, F, nf, a.ld);
     auto go = [&](auto FM) {
@@ -2242,6 +2246,7 @@ void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     else go(IC<SPM_CSR>{});
 }
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 1, a.kmax, TK_A1_SCALAR ? 0 : 2);
     with_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
@@ -2251,12 +2256,14 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     });
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_a2<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
 }
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 3, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_finalize<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
@@ -2269,11 +2276,13 @@ static void with_band_fmt(int fmt, F f) {
     else f(IC<SPM_DIA>{});
 }
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     with_band_fmt(a.fmt, [&](auto FM) {
         hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
     });
 }
 void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
     const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
     with_band_fmt(a.fmt, [&](auto FM) {
@@ -2284,6 +2293,7 @@ void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s
     });
 }
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
@@ -2298,12 +2308,14 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     });
 }
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(1, a.kmax, 0);
     with_fmt(a.fmt, [&](auto FM) {
         hipLaunchKernelGGL((k_lan_l1_plain<decltype(FM)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
 }
 void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
     const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
     const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
@@ -2314,15 +2326,18 @@ void launch_lan_d1(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     });
 }
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 3, a.kmax, 0);
     with_fmt(a.fmt, [&](auto FM) {
         hipLaunchKernelGGL((k_lan_l1_fused<decltype(FM)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
     });
 }
 void launch_lan_l2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     hipLaunchKernelGGL(k_lan_l2, dim3(a.npart, nf), dim3(TPB), lds_bytes(1, a.kmax, 0), s, F, a);
 }
 void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int nc = a.j + 1;
     const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
     const size_t lds = (size_t)((M + 15) / 16 + 1) * TPB * sizeof(double);
@@ -2334,6 +2349,7 @@ void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s
     });
 }
 void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int nc = a.j + 1;
     const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
     const size_t lds = ((size_t)((M + 15) / 16 + 1) * TPB + (size_t)t * ldy) * sizeof(double);   // acc + Y_s
@@ -2343,10 +2359,12 @@ void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, doubl
     });
 }
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ,
                    const KArgs* ax) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     KArgs none;
     memset(&none, 0, sizeof(none));
     if (npart <= 0 && !gate)
@@ -2377,6 +2395,7 @@ void launch_mirror_records(const double* src, double* dst, int cnt, unsigned lon
 }
 
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t hb = (size_t)(a.kmax + 1) * (a.kmax + 2);
     size_t lds = (kind == POST_ARN && hb <= POST_LDS_MAX) ? hb * sizeof(double) : 0;
     if (kind == POST_ARN_D) lds = bk_lds_doubles(a.j) * sizeof(double);
@@ -2384,6 +2403,7 @@ void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int 
 }
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     // NG = 16-column groups per block: t <= 16 -> 1, <= 32 -> 2, else 2 per z-slice
     if (t <= 16)
         hipLaunchKernelGGL(k_basis_mul<1>, dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t);

@@ -76,7 +76,7 @@ class TensorDecomposition:
         self._dmats = list(mats.values())
         self.dev = DeviceDecomposition(self.ctx, self.method, self.d, self.part.first, dmats,
                                        [b[s] for s in self.part.local()], self.kmax,
-                                       track_all_gram=self.track_all_gram)
+                                       track_all_gram=self.track_all_gram, n=len(b[0]))
 
     # -------------------------------------------------------------- records -> host mirror
     def _apply_gram(self, rec):

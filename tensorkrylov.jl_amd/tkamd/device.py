@@ -103,13 +103,15 @@ class DeviceDecomposition:
     """tk_decomp: this rank's factors s = first .. first+nf-1 of a d_total-factor
     tensor decomposition, with device-resident V_s (n x kmax+1), b_s and work vectors."""
 
-    def __init__(self, ctx, method, d_total, first, mats, bs, kmax, track_all_gram=False):
+    def __init__(self, ctx, method, d_total, first, mats, bs, kmax, track_all_gram=False, n=None):
+        """mats may be empty (a rank of a job with more ranks than factors: it only takes part
+        in the records exchange); n is then required."""
         self.ctx = ctx
         self.method = method
         self.d_total = d_total
         self.first = first
         self.nf = len(mats)
-        self.n = mats[0].n
+        self.n = mats[0].n if mats else int(n)
         self.kmax = kmax
         self.layout = L.RecordLayout(kmax)
         self.m = self.layout.m
@@ -174,6 +176,9 @@ class DeviceDecomposition:
 
     def basis_mul(self, k, Ys, want=True):
         """X_s = V_s[:, :k] @ Y_s for the local factors (Ys: list of k x t arrays)."""
+        if self.nf == 0:   # (still the flush, and its record exchange, every rank makes)
+            self.flush(False)
+            return [] if want else None
         t = Ys[0].shape[1]
         Y = np.ascontiguousarray(np.stack([np.asarray(y, dtype=np.float64).T for y in Ys]))  # [nf][t][k]
         X = np.zeros((self.nf, t, self.n)) if want else None

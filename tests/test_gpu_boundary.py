@@ -119,3 +119,29 @@ def test_failed_step_refuses_later_steps_and_destroys(ctx, monkeypatch):
     dev.close()
     A.close()
     c2.close()
+
+
+@pytest.mark.parametrize("comm", [False, True])
+def test_rank_without_factors(ctx, comm, monkeypatch):
+    """A rank of a job with more ranks than factors (d < N) owns no factor: create, init, the
+    sweep, the flush and the records exchange run with every launch skipped, and its records
+    are all zero (the all-reduce adds nothing) -- forced through the RCCL path on a 1-rank
+    communicator too."""
+    tk = _tk()
+    n, K, d = 3000, 12, 3
+    c = ctx
+    if comm:
+        c = tk.Context(0)
+        c.init_comm(tk.unique_id(), 1, 0)
+        monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    for method in (0, 1, 2):
+        dev = tk.DeviceDecomposition(c, method, d, d, [], [], K, n=n)
+        rec0 = dev.init()
+        dev.sweep(0, K)
+        assert dev.basis_mul(K, [], want=True) == []
+        recs = dev.records(0, K + 2)
+        dev.close()
+        assert not np.any(rec0)
+        assert not np.any(recs)
+    if comm:
+        c.close()
