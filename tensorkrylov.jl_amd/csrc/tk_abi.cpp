@@ -1422,7 +1422,9 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
     // done in the same launch as V*Y (each basis tile streamed once for both)
     const int jl = dc->last_j;
     const char* nofuse = getenv("TKHIP_NO_FUSED_FLUSH");
-    const bool fuse = dc->pending && dc->method == TK_ARNOLDI && dc->fin_d && jl + 1 <= D1_JMAX &&
+    // (the one-sweep Lanczos' pending column too: its flush reads the same register row)
+    const bool lan1 = dc->method == TK_LANCZOS && dc->onesweep && jl <= ARN_D1_JMAX;
+    const bool fuse = dc->pending && (dc->method == TK_ARNOLDI || lan1) && dc->fin_d && jl + 1 <= D1_JMAX &&
                       k <= jl + 1 && !(nofuse && nofuse[0] == '1');
     const int ldy = fuse ? 64 : k;   // fused: Y_s columns zero-padded to the register row's width
     if (dc->pending && !fuse) {
@@ -1464,9 +1466,14 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
             f.ubuf = (jl & 1) ? 0 : 1;
             f.ecol = (jl & 1) ? -1 : jl;
         }
-        RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, s), "fin_vy");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 3, jl + 3, dc->ntiles, s), "reduce");
-        RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");
+        RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, lan1 ? 2 : 0, s), "fin_vy");
+        if (lan1) {
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 1, jl + 3, dc->ntiles, s), "reduce");
+            RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_LAN_FIN, 0, 1, s), "post");
+        } else {
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, 3, jl + 3, dc->ntiles, s), "reduce");
+            RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");
+        }
         dc->pending = false;
         st = exchange_and_copy(dc, slot, nullptr);
         if (st) return st;

@@ -127,7 +127,8 @@ constexpr int ARN_D1_JMAX = 63;
 // launchers (tk_kernels.hip)
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
                            unsigned long long seq, hipStream_t s);
-void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s);
+void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, int mode,
+                   hipStream_t s);
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);

@@ -1264,7 +1264,7 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     // MODE 2 (one-sweep Lanczos): v = inv(beta) .* (u - alpha v_j), u = the last step's raw vector
     const double alpha2 = MODE == 2 ? ld(d.sc, SC_ALPHA) : 0.0;
     const double up2 = MODE == 2 ? ld(a.ubuf ? d.W : d.U, r) : 0.0;
-    if (MODE >= 1 && !gram) {
+    if (MODE >= 1 && !gram && !VY) {
         // Lanczos without a Gram row: v, the pair store (other half = column j), <v,b>
         const double vjc = em ? (ok ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j));
         double v;
@@ -2144,7 +2144,7 @@ __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, K
 // The pending column's flush (fin_d_tile, MODE 0: Arnoldi) and V * Y of the same tile in one
 // block: the register row the flush loads also feeds the product, so each basis tile is
 // streamed from HBM once for both.  Y: [nf][t][ldy] with zero rows k..ldy-1, k <= j + 1.
-template <int MAXC>
+template <int MAXC, int MODE>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= TK_VY_OCC4 ? 4 : 3, MAXC <= TK_VY_OCC4 ? 4 : 3)))
 void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Yall, double* __restrict__ Xall,
               int ldy, int t) {
@@ -2153,7 +2153,7 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
     const DFac& d = F[f];
     const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
     if (slot >= a.ntiles) return;
-    fin_d_tile<MAXC, 0, true>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
+    fin_d_tile<MAXC, MODE, true>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
 }
 
 // ------------------------------------------------------------------ plain SpMV (test hook)
@@ -2348,14 +2348,16 @@ void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s
         else hipLaunchKernelGGL((k_fin_d<decltype(Mc)::value, 2>), grid, dim3(TPB), lds, s, F, a);
     });
 }
-void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, hipStream_t s) {
+void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, int mode,
+                   hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int nc = a.j + 1;
     const int M = nc <= 8 ? 8 : (nc + 7) / 8 * 8;
     const size_t lds = ((size_t)((M + 15) / 16 + 1) * TPB + (size_t)t * ldy) * sizeof(double);   // acc + Y_s
     const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
     with_maxc(nc, [&](auto Mc) {
-        hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
+        if (mode == 2) hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 2>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
+        else hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 0>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
     });
 }
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {

@@ -407,8 +407,9 @@ def test_arnoldi_untracked_factors_identical(ctx, orth, monkeypatch):
 
 
 
+@pytest.mark.parametrize("method", ["arnoldi", "lanczos"])
 @pytest.mark.parametrize("cls,n,t", [("Laplace", 3000, 17), ("ConvDiff", 5000, 3), ("Laplace", 1000, 30)])
-def test_fused_flush_basis_mul_identical(ctx, cls, n, t, monkeypatch):
+def test_fused_flush_basis_mul_identical(ctx, cls, n, t, method, monkeypatch):
     """basis_mul on a pending column finalizes it in the same launch as V*Y (k_fin_vy: the
     product from the flush's register row, FP64 FMAs); the flushed column, its record (Gram
     row, b-tilde) and the columns before it are bitwise those of the separate flush +
@@ -427,7 +428,8 @@ def test_fused_flush_basis_mul_identical(ctx, cls, n, t, monkeypatch):
         else:
             monkeypatch.setenv("TKHIP_NO_FUSED_FLUSH", "1")
         A = tk.DeviceMatrix(ctx, csc)
-        dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, 3, 0, [A] * 3, bs, K, track_all_gram=True)
+        mcode = tk._lib.TK_ARNOLDI if method == "arnoldi" else tk._lib.TK_LANCZOS
+        dev = tk.DeviceDecomposition(ctx, mcode, 3, 0, [A] * 3, bs, K, track_all_gram=method == "arnoldi")
         dev.init(False)
         dev.sweep(0, K)
         X = dev.basis_mul(K, Ys)
