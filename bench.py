@@ -93,6 +93,9 @@ def main():
                     help="diagnostic: on 1 GPU run only rank 0's factor block of an N-rank "
                          "partition (records exchanged over a 1-rank communicator) to predict "
                          "the per-GPU step time at N GPUs; the JSON line is marked as emulated")
+    ap.add_argument("--emulate-rank", type=int, default=0,
+                    help="with --emulate-ranks: which rank's factor block to run (default 0, "
+                         "the rank holding the tracked factor 1)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the (untimed) full-driver measurement reported as end_to_end")
     ap.add_argument("--pmc-mode", action="store_true",
@@ -115,7 +118,7 @@ def main():
     ctx = tkamd.Context(local_rank)
     part = tkamd.Partition(d, world, rank)
     if args.emulate_ranks > 1 and world == 1:
-        part = tkamd.Partition(d, args.emulate_ranks, 0)
+        part = tkamd.Partition(d, args.emulate_ranks, args.emulate_rank)
         args.force_comm = os.environ.get("TK_EMULATE_NOCOMM") != "1"
     uid_path = None
     if world > 1:

@@ -440,6 +440,17 @@ __device__ __forceinline__ void stage(double* dst, const double* src, int nc, in
 
 __device__ __forceinline__ double ld(const double* p, int64_t i) { return GP(const double, p)[i]; }
 __device__ __forceinline__ void st(double* p, int64_t i, double v) { GP(double, p)[i] = v; }
+// X_s = V_s Y_s (written once, read by the host copy-out): streaming stores
+#ifndef TK_X_NT
+#define TK_X_NT 1
+#endif
+__device__ __forceinline__ void st_x(double* p, int64_t i, double v) {
+#if TK_X_NT
+    __builtin_nontemporal_store(v, &GP(double, p)[i]);
+#else
+    GP(double, p)[i] = v;
+#endif
+}
 
 // y[r] = sum over row r of A, terms in ascending column order, products and sums
 // separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
@@ -1323,8 +1334,8 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
             // so the stores stream (column-major n x t stores cost a third of the kernel)
             if (ok && !(TK_VY_TEST & 1)) {
                 double* Xt = Xf + (int64_t)slot * TPB * tq + t;
-                st(Xt, (int64_t)q * TPB, x0);
-                if (q + 1 < tq) st(Xt, (int64_t)(q + 1) * TPB, x1);
+                st_x(Xt, (int64_t)q * TPB, x0);
+                if (q + 1 < tq) st_x(Xt, (int64_t)(q + 1) * TPB, x1);
             }
         }
     }
@@ -2126,7 +2137,7 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
         if (r < a.n) {
             const int cn = min(16, tn - 16 * q);
             for (int c = 0; c < cn; ++c)   // X tile-major (as k_fin_vy)
-                st(X, (int64_t)tile * TPB * t + (int64_t)(t0 + 16 * q + c) * TPB + threadIdx.x, Xs[c * XS_STRIDE + threadIdx.x]);
+                st_x(X, (int64_t)tile * TPB * t + (int64_t)(t0 + 16 * q + c) * TPB + threadIdx.x, Xs[c * XS_STRIDE + threadIdx.x]);
         }
     }
 }
