@@ -568,13 +568,28 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 // Uint rows are padded to ilv_pitch(nf) doubles (a power of two: one aligned 16..64-byte
 // piece per gather, read as 16-byte loads)
 __host__ __device__ inline int ilv_pitch(int nf) { return nf <= 2 ? 2 : (nf <= 4 ? 4 : 8); }
+// One 256-row tile per block (ld_ is a multiple of 256): the factors' entries are transposed
+// through LDS so every wave store writes 1 KiB of contiguous Uint (row-strided 16-byte
+// stores left each line to be completed by four separate instructions)
 __global__ __launch_bounds__(TPB) void k_ilv(const DFac* __restrict__ F, int nf, int64_t ld_) {
-    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
-    if (r >= ld_) return;
+    __shared__ double tl[TPB * 9];   // row pitch 9: the transposing writes are conflict-free
+    const int64_t r0 = (int64_t)blockIdx.x * TPB;
+    const int t = threadIdx.x;
     double* Ui = F[0].Uint;
     const int p = ilv_pitch(nf);
-    for (int f = 0; f < p; f += 2)   // 16-byte stores
-        GP(d2_t, Ui + r * p)[f >> 1] = (d2_t){f < nf ? ld(F[f].U, r) : 0.0, f + 1 < nf ? ld(F[f + 1].U, r) : 0.0};
+    double u[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) u[f] = f < nf ? ld(F[f < nf ? f : 0].U, r0 + t) : 0.0;
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+        if (f < p) tl[t * 9 + f] = u[f];
+    __syncthreads();
+    const int nch = TPB * p / 2;   // 16-byte pieces of the tile's Uint rows
+    auto* out = GP(d2_t, Ui + r0 * p);
+    for (int c = t; c < nch; c += TPB) {
+        const int e = 2 * c, row = e / p, col = e - row * p;
+        out[c] = (d2_t){tl[row * 9 + col], tl[row * 9 + col + 1]};
+    }
 }
 template <int FMT, int NFM>
 __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int nf, KArgs a) {
