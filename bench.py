@@ -118,7 +118,7 @@ def main():
     ctx = tkamd.Context(local_rank)
     part = tkamd.Partition(d, world, rank)
     if args.emulate_ranks > 1 and world == 1:
-        part = tkamd.Partition(d, args.emulate_ranks, args.emulate_rank)
+        part = tkamd.Partition(d, args.emulate_ranks, args.emulate_rank, term_split=False)
         args.force_comm = os.environ.get("TK_EMULATE_NOCOMM") != "1"
     uid_path = None
     if world > 1:
@@ -139,6 +139,8 @@ def main():
              "TensorLanczosReorth": L.TK_LANCZOS_REORTH}[method]
     dev = tkamd.DeviceDecomposition(ctx, mcode,
                                     d, part.first, [A] * part.nf, bs, K, n=n)
+    if part.replica:        # more ranks than factors: this rank's factor is another rank's replica
+        dev.set_replica()
     # exp-sum rank at k = K (Laplace: kappa independent of n and d)
     sym = inst == "SymInstance"
     if sym and cls == "Laplace":
@@ -151,7 +153,10 @@ def main():
     else:
         t_rank = 17 if sym else 3
     rng = np.random.default_rng(7)
-    Ys = [rng.standard_normal((K, t_rank)) for _ in range(part.nf)]
+    # this rank's slice of the t exp-sum terms (all of them unless replicas split the terms)
+    tc0, tc1 = part.terms(t_rank)
+    Ys = [rng.standard_normal((K, t_rank))[:, tc0:tc1] for _ in range(part.nf)]
+    t_loc = tc1 - tc0
     sweeps = dev.arnoldi_sweeps if method in ("TensorArnoldi", "TensorLanczos") else 0
 
     host_issue = [0.0, 0]
@@ -282,8 +287,8 @@ def main():
     # the same steps priced in the reference algorithm's bytes (MGS2 streams V
     # twice per step): what a two-sweep implementation would have to move at this rate
     ref_step = sum(alg_bytes_step(n, nnz, k, method, 2) for k in range(1, K + 1)) * part.nf
-    vy_bytes = (8 * n * K + 8 * K * t_rank + 8 * n * t_rank) * part.nf
-    vy_flops = 2 * n * K * t_rank * part.nf
+    vy_bytes = (8 * n * K + 8 * K * t_loc + 8 * n * t_loc) * part.nf
+    vy_flops = 2 * n * K * t_loc * part.nf
     vy_s = (vy_ms / 1e3) / max(vy_cnt, 1)
     mf_s = (mf_ms / 1e3) / max(mf_cnt, 1)
     fused_vy = method == "TensorArnoldi"      # the step's basis_mul finalizes the pending column with it
@@ -320,8 +325,10 @@ def main():
                                    "step = 1 sweep of K iterations + V*Y (t=%d)"
                                    % (args.config, d, n, cls, method, K, world, t_rank),
                        "d": d, "n_s": n, "nmax": K, "matrix": cls, "method": method,
-                       "parallelism": "factor-partition x%d (RCCL all-reduce of records per iteration%s)"
-                                      % (world, ", forced on 1 rank" if args.force_comm else "")},
+                       "parallelism": "factor-partition x%d (RCCL all-reduce of records per iteration%s%s)"
+                                      % (world, ", forced on 1 rank" if args.force_comm else "",
+                                         "; ranks >= d replicate a factor and split its V*Y terms"
+                                         if part.term_split else "")},
             "roofline": {
                 "bound": "hbm",
                 "kernel": ("one-sweep Arnoldi factor-step (k_arn_d1: v_j, two SpMVs from LDS, CGS projections "

@@ -130,6 +130,15 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc);
  * per step or there is no exchange (single rank; TK_LANCZOS_REORTH; TKHIP_XCH_EVENTS=1). */
 int tk_decomp_exchange_signalled(tk_decomp* dc);
 
+/* Exp-sum-term split (more ranks than factors): a rank holding a REPLICA of
+ * factors another rank owns runs the same steps (bitwise the same basis) but sends zero rows
+ * into the records all-reduce, so every factor's record is counted once; at convergence each
+ * replica forms its own slice of the t columns of X_s = V_s Y_s (tk_decomp_basis_mul with
+ * Y_s[:, c0:c1]), i.e. basis_tensor_mul! (src/utils.jl:478-488) over the exponential-sum
+ * terms of src/tensor_krylov_method.jl:10-34.  Call before tk_decomp_init; needs a handle
+ * with a records exchange (TK_ERR_STATE otherwise).  replica = 0 is a no-op. */
+tk_status tk_decomp_set_replica(tk_decomp* dc, int replica);
+
 /* Per-factor record layout (doubles; m = tk_record_len(kmax)), written by every step:
  *   [0 .. kmax+1]        H[0..j+1, j] as computed by this step (rest 0)
  *   [kmax+2 .. 2kmax+3]  Gram row G[c, 0..c] = V[:,c]' V[:,0..c] of column c below

@@ -597,6 +597,9 @@ struct tk_decomp {
     std::vector<void*> allocs;
     double* rec = nullptr;   // send records [(kmax+2) slots][d_total][m] (local rows only)
     double* recv = nullptr;  // all-reduced records (== rec on a single rank)
+    // replica of factors another rank owns (exp-sum-term split, tk_decomp_set_replica): the
+    // all-reduce sends these zero rows instead of rec, so every record is counted once
+    double* zrec = nullptr;
     double* Ydev = nullptr; size_t ycap = 0;
     double* Xdev = nullptr; size_t xcap = 0;
     double* scratch = nullptr;   // column gather buffer (n x 8)
@@ -861,6 +864,23 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
 
 int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
 
+tk_status tk_decomp_set_replica(tk_decomp* dc, int replica) { TK_API_BEGIN
+    CHECKARG(dc, "NULL handle");
+    if (dc->inited) return fail(TK_ERR_STATE, "tk_decomp_set_replica: after tk_decomp_init");
+    if (!replica) return TK_OK;
+    if (dc->recv == dc->rec)
+        return fail(TK_ERR_STATE, "tk_decomp_set_replica: a replica needs a records exchange (multi-rank communicator)");
+    if (!dc->zrec) {
+        HIPCHK(hipSetDevice(dc->ctx->device));
+        void* p = nullptr;
+        tk_status st = dalloc(dc, &p, (size_t)(dc->kmax + 2) * dc->d_total * dc->m * sizeof(double));
+        if (st) return st;
+        dc->zrec = (double*)p;
+    }
+    return TK_OK;
+    TK_API_END
+}
+
 int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
     if (!dc) return 0;
     if (dc->method == TK_LANCZOS) return dc->onesweep ? 1 : 0;
@@ -926,7 +946,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
 static tk_status exchange_range(tk_decomp* dc, int s0, int s1, bool signalled) {
     tk_ctx* c = dc->ctx;
     const size_t cnt = (size_t)dc->d_total * dc->m;
-    double* s = dc->rec + (size_t)s0 * cnt;
+    double* s = (dc->zrec ? dc->zrec : dc->rec) + (size_t)s0 * cnt;
     double* r = dc->recv + (size_t)s0 * cnt;
     const size_t tot = cnt * (size_t)(s1 - s0 + 1);
     // the exchange runs on its own stream, overlapping the next steps' kernels; it starts

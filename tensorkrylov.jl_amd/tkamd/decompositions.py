@@ -16,13 +16,27 @@ from .device import Context, DeviceDecomposition, DeviceMatrix
 
 class Partition:
     """Contiguous factor blocks over ranks: the first d % N ranks own
-    ceil(d/N) factors, the rest floor(d/N)."""
+    ceil(d/N) factors, the rest floor(d/N).
 
-    def __init__(self, d, nranks=1, rank=0):
+    With more ranks than factors (N > d) and term_split (default; TKHIP_TERM_SPLIT=0 turns
+    it off), rank r >= d holds a REPLICA of factor r % d instead of idling: it runs the same
+    steps (sending zero rows into the records all-reduce, tk_decomp_set_replica) and at
+    convergence the ranks holding factor s split the t exponential-sum terms of
+    X_s = V_s Y_s between them (terms(t); src/tensor_krylov_method.jl:10-34 and
+    basis_tensor_mul!, src/utils.jl:478-488).  Without term_split those ranks own nothing."""
+
+    def __init__(self, d, nranks=1, rank=0, term_split=None):
+        import os
         self.d, self.nranks, self.rank = d, nranks, rank
+        if term_split is None:
+            term_split = os.environ.get("TKHIP_TERM_SPLIT", "1") != "0"
+        self.term_split = bool(term_split) and nranks > d
         q, r = divmod(d, nranks)
         self.sizes = [q + (1 if i < r else 0) for i in range(nranks)]
         self.starts = [sum(self.sizes[:i]) for i in range(nranks)]
+        if self.term_split:
+            self.sizes = [1] * nranks
+            self.starts = [i % d for i in range(nranks)]
 
     @property
     def first(self):
@@ -32,8 +46,25 @@ class Partition:
     def nf(self):
         return self.sizes[self.rank]
 
+    @property
+    def replica(self):
+        """True when another rank owns this rank's factors (their records come from there)."""
+        return self.term_split and self.rank >= self.d
+
     def local(self):
         return range(self.first, self.first + self.nf)
+
+    def terms(self, t):
+        """This rank's contiguous slice [c0, c1) of the t exponential-sum terms (columns of
+        Y_s / X_s): all of them unless term_split, else the ranks holding the same factor
+        (ranks s, s + d, s + 2d, ...) take near-equal consecutive slices (possibly empty)."""
+        if not self.term_split:
+            return 0, t
+        s, g = self.rank % self.d, self.rank // self.d
+        groups = len(range(s, self.nranks, self.d))
+        q, r = divmod(t, groups)
+        c0 = g * q + min(g, r)
+        return c0, c0 + q + (1 if g < r else 0)
 
 
 class TensorDecomposition:
@@ -63,6 +94,8 @@ class TensorDecomposition:
     def _attach(self, b):
         if self._backend is not None:           # injected (tests of the host logic only)
             self.dev = self._backend(self, b)
+            if self.part.replica:
+                self.dev.set_replica()
             return
         if self.ctx is None:
             self.ctx = Context(0)
@@ -77,6 +110,8 @@ class TensorDecomposition:
         self.dev = DeviceDecomposition(self.ctx, self.method, self.d, self.part.first, dmats,
                                        [b[s] for s in self.part.local()], self.kmax,
                                        track_all_gram=self.track_all_gram, n=len(b[0]))
+        if self.part.replica:
+            self.dev.set_replica()
 
     # -------------------------------------------------------------- records -> host mirror
     def _apply_gram(self, rec):

@@ -139,6 +139,11 @@ class DeviceDecomposition:
         """Records exchange triggered by a signal word, not an event (tk_decomp_exchange_signalled)."""
         return bool(self.ctx._lib.tk_decomp_exchange_signalled(self.h))
 
+    def set_replica(self, on=True):
+        """This rank's factors are replicas of another rank's (tk_decomp_set_replica): same
+        steps, zero rows sent into the records all-reduce."""
+        L.check(self.ctx._lib.tk_decomp_set_replica(self.h, 1 if on else 0))
+
     def _rec(self):
         return np.zeros((self.d_total, self.m))
 
@@ -176,9 +181,12 @@ class DeviceDecomposition:
 
     def basis_mul(self, k, Ys, want=True):
         """X_s = V_s[:, :k] @ Y_s for the local factors (Ys: list of k x t arrays)."""
-        if self.nf == 0:   # (still the flush, and its record exchange, every rank makes)
+        if self.nf == 0 or Ys[0].shape[1] == 0:
+            # (still the flush, and its record exchange, every rank makes); an empty term slice
             self.flush(False)
-            return [] if want else None
+            if not want:
+                return None
+            return [np.zeros((self.n, 0)) for _ in Ys] if self.nf else []
         t = Ys[0].shape[1]
         Y = np.ascontiguousarray(np.stack([np.asarray(y, dtype=np.float64).T for y in Ys]))  # [nf][t][k]
         X = np.zeros((self.nf, t, self.n)) if want else None

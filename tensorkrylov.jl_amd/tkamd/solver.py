@@ -34,7 +34,8 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
                  threads=None, overlay=None):
     """tensorkrylov!(convergence_data, A, b, tol, nmax, orthonormalization_type).
     Returns the approximate solution as a KruskalTensor of the LOCAL factors
-    (x_s = V_s y_s) on convergence, else None.
+    (x_s = V_s y_s; with a term-splitting Partition only this rank's slice x.terms of the
+    t exponential-sum terms) on convergence, else None.
 
     pipelined: steps k+1 .. k+depth are enqueued on the device before the host evaluates
     iteration k (compressed solve, residual), so device and host work overlap and the
@@ -116,10 +117,7 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             if rel < tol:                                           # :108-118
                 # basis_tensor_mul! on the device; X sized by ncomponents(y)
                 # (the reference sizes it by approxdata.rank, SURVEY.md 3.2 deviation)
-                loc = list(td.part.local())
-                X = td.dev.basis_mul(k, [Ys[s] for s in loc])
-                x = KruskalTensor(lam.copy(), X)
-                x.factors = loc
+                x = _solution(td, k, lam, Ys)
                 conv.timing["loop_s"] = time.perf_counter() - t_loop
                 if verbose:
                     print("Convergence")
@@ -133,6 +131,19 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             conv.decomposition = td
         else:
             td.close()
+
+
+def _solution(td, k, lam, Ys):
+    """basis_tensor_mul! (src/utils.jl:478-488) on the device for this rank's factors and its
+    slice [c0, c1) of the exponential-sum terms (all t unless the partition splits terms
+    between replicas): x.factors / x.terms say which part of the Kruskal tensor this is."""
+    loc = list(td.part.local())
+    c0, c1 = td.part.terms(len(lam))
+    X = td.dev.basis_mul(k, [np.asarray(Ys[s])[:, c0:c1] for s in loc])
+    x = KruskalTensor(lam[c0:c1].copy(), X)
+    x.factors = loc
+    x.terms = (c0, c1)
+    return x
 
 
 def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, threads, t_loop):
@@ -167,10 +178,7 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
     x = None
     if outcome == 1:                                                # :108-118
         lam, Ys = sv.solution(k_end)
-        loc = list(td.part.local())
-        X = td.dev.basis_mul(k_end, [Ys[s] for s in loc])
-        x = KruskalTensor(lam.copy(), X)
-        x.factors = loc
+        x = _solution(td, k_end, lam, Ys)
     conv.timing["loop_s"] = time.perf_counter() - t_loop
     # the host mirror of H, b~ and factor 1's Gram rows (principal_minors readers)
     H, bt, G = sv.state()

@@ -22,16 +22,20 @@ class FakeDecomposition:
         self.method = td.name
         self.b = {s: np.asarray(b[s], dtype=np.float64) for s in self.loc}
         self.f = {s: O.Factor(td.A[s], self.b[s], td.kmax) for s in self.loc}
+        self.replica = False
 
-    @staticmethod
-    def _exchange(r):
+    def set_replica(self):
+        self.replica = True
+
+    def _exchange(self, r):
         import sys
         if "torch.distributed" not in sys.modules:   # single process: nothing to sum
             return r
         import torch.distributed as dist
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             import torch
-            t = torch.from_numpy(r)
+            # a replica sends zero rows (tk_decomp_set_replica); it receives everyone's
+            t = torch.from_numpy(np.zeros_like(r) if self.replica else r)
             dist.all_reduce(t)
             return t.numpy()
         return r

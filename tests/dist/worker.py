@@ -20,19 +20,27 @@ from _fake_device import backend  # noqa: E402
 
 def main():
     out, method, d, K = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    n = int(sys.argv[5]) if len(sys.argv) > 5 else 200
+    tol = float(sys.argv[6]) if len(sys.argv) > 6 else 1e-9
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    n = 200
     rng = np.random.default_rng(777)
-    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    if len(sys.argv) > 7 and sys.argv[7] == "shared":    # random_rhs (src/system.jl:5-11)
+        bs = rng.random(n)
+        b = [bs / np.linalg.norm(bs) for _ in range(d)]
+    else:
+        b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
     A = tkamd.KroneckerMatrix.gallery(tkamd.SymInstance, d, n, tkamd.Laplace)
     conv = tkamd.ConvergenceData(K)
     part = tkamd.Partition(d, world, rank)
-    x = tkamd.tensorkrylov(conv, A, b, 1e-9, K, method, partition=part, backend=backend)
+    x = tkamd.tensorkrylov(conv, A, b, tol, K, method, partition=part, backend=backend)
     res = {"rank": rank, "world": world, "local": list(part.local()),
            "relres": conv.relative_residual_norm.tolist(), "proj": conv.projected_residual_norm.tolist(),
            "orth": conv.orthogonality_data.tolist(), "niter": conv.niterations,
-           "x_factors": None if x is None else x.factors}
+           "x_factors": None if x is None else x.factors,
+           "x_terms": None if x is None else list(x.terms),
+           "x_lam": None if x is None else x.lam.tolist(),
+           "x_fmat": None if x is None else [f.tolist() for f in x.fmat]}
     with open("%s.%d.json" % (out, rank), "w") as f:
         json.dump(res, f)
     dist.barrier()

@@ -145,3 +145,53 @@ def test_rank_without_factors(ctx, comm, monkeypatch):
         assert not np.any(recs)
     if comm:
         c.close()
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_replica_sends_zero_rows_and_splits_terms(ctx, method, monkeypatch):
+    """Exp-sum-term split (tk_decomp_set_replica; more ranks than factors): a replica runs the
+    owner's steps -- its basis is the owner's bit for bit -- but sends zero rows into the
+    records all-reduce (on a 1-rank communicator every received record is zero), and V*Y on
+    a slice Y[:, c0:c1] of the terms is the owner's X[:, c0:c1].  set_replica is refused on a
+    handle without a records exchange and after init."""
+    tk = _tk()
+    n, K, d, t = 3000, 12, 2, 7
+    csc = tk.assemble_matrix(n, "Laplace")
+    rng = np.random.default_rng(5)
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    Y = [rng.standard_normal((K, t)) for _ in range(d)]
+    A0 = tk.DeviceMatrix(ctx, csc)
+    own = tk.DeviceDecomposition(ctx, method, d, 0, [A0] * d, bs, K)
+    with pytest.raises(tk.TKError, match="replica needs"):
+        own.set_replica()
+    own.init(False)
+    own.sweep(0, K)
+    Xo = own.basis_mul(K, Y)
+    Vo = [own.basis(f, 0, K + 1) for f in range(d)]
+    own.close()
+    A0.close()
+
+    c = tk.Context(0)
+    c.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    A1 = tk.DeviceMatrix(c, csc)
+    rep = tk.DeviceDecomposition(c, method, d, 0, [A1] * d, bs, K)
+    rep.set_replica()
+    rec0 = rep.init()
+    with pytest.raises(tk.TKError, match="after tk_decomp_init"):
+        rep.set_replica()
+    rep.sweep(0, K)
+    c0, c1 = 2, 6
+    Xr = rep.basis_mul(K, [y[:, c0:c1] for y in Y])
+    recs = rep.records(0, K + 1)
+    Vr = [rep.basis(f, 0, K + 1) for f in range(d)]
+    empty = rep.basis_mul(K, [y[:, :0] for y in Y])        # an empty slice of the terms
+    rep.close()
+    A1.close()
+    c.close()
+    assert not np.any(rec0) and not np.any(recs)
+    for f in range(d):
+        assert np.array_equal(Vr[f], Vo[f])
+        ref = Xo[f][:, c0:c1]
+        assert Xr[f].shape == ref.shape and empty[f].shape == (n, 0)
+        assert np.abs(Xr[f] - ref).max() <= 1e-14 * np.abs(ref).max()
