@@ -158,6 +158,10 @@ def main():
     Ys = [rng.standard_normal((K, t_rank))[:, tc0:tc1] for _ in range(part.nf)]
     t_loc = tc1 - tc0
     sweeps = dev.arnoldi_sweeps if method in ("TensorArnoldi", "TensorLanczos") else 0
+    if world > 1:
+        preflight(ctx, world, rank, {"d": d, "n_s": n, "K": K, "method": mcode, "world": world,
+                                     "t": t_rank, "config": sorted(CONFIGS).index(args.config),
+                                     "steps": args.steps, "warmup": args.warmup})
 
     host_issue = [0.0, 0]
 
@@ -393,6 +397,21 @@ def toeplitz_bytes(csc):
     return 0
 
 
+def preflight(ctx, world, rank, fields):
+    """Before the first sweep: every rank must run the same workload (a rank with other
+    sizes would issue all-reduces of other lengths and hang the job).  Each rank writes its
+    values into its own row, one RCCL all-reduce (bounded by TKHIP_WAIT_S) gives every rank
+    every row, and any difference ends the run on all ranks with the table."""
+    names = list(fields)
+    rows = np.zeros((world, len(names)))
+    rows[rank] = [float(fields[k]) for k in names]
+    rows = ctx.allreduce_host(rows.ravel()).reshape(world, len(names))
+    bad = [k for i, k in enumerate(names) if not np.all(rows[:, i] == rows[0, i])]
+    if bad:
+        sys.exit("bench preflight: ranks disagree on %s: %s" % (
+            ", ".join(bad), {k: rows[:, names.index(k)].tolist() for k in bad}))
+
+
 def exchange_uid(tkamd, rank, timeout=120.0):
     """Hand the RCCL unique id from rank 0 to the other ranks of this node through a
     file keyed by the launcher's pid (all ranks of one torch.distributed.run share it)."""
@@ -436,4 +455,14 @@ def cpu_baseline(csc, n, d, K, seconds):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:   # noqa: BLE001
+        # a libtkhip error (e.g. TK_ERR_RCCL: a peer never joined an all-reduce within
+        # TKHIP_WAIT_S) ends THIS rank with its diagnosis; exit without running destructors,
+        # which could wait on the same peer
+        if type(e).__name__ != "TKError":
+            raise
+        sys.stderr.write("bench.py rank %s: %s\n" % (os.environ.get("RANK", "0"), e))
+        sys.stderr.flush()
+        os._exit(3)

@@ -130,6 +130,25 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc);
  * per step or there is no exchange (single rank; TK_LANCZOS_REORTH; TKHIP_XCH_EVENTS=1). */
 int tk_decomp_exchange_signalled(tk_decomp* dc);
 
+/* The next step j that tk_decomp_step accepts (steps 0 .. j-1 are enqueued; a driver that
+ * ran ahead, like tk_solver_run, may have enqueued more steps than its caller has read). */
+int tk_decomp_next_step(tk_decomp* dc);
+
+/* Element-wise max of vals[0..count) over the ranks sharing dc's records exchange (no-op on
+ * one rank; count <= 64).  Collective: every rank calls it at the same point of its call
+ * sequence.  tk_solver_run agrees its issue depth and worker count with it, so that every
+ * rank issues the same sequence of steps, record reads and therefore all-reduces. */
+tk_status tk_decomp_agree(tk_decomp* dc, int* vals, int count);
+
+/* Multi-rank waits (the records exchange, tk_comm_allreduce_host, tk_ctx_sync, destroy) are
+ * bounded by TKHIP_WAIT_S seconds (default 120): on expiry the call returns TK_ERR_RCCL naming
+ * the record slot / step it waited for and RCCL's asynchronous error state, and the context
+ * is marked unusable (later collectives fail at once; its device buffers are left to process
+ * exit, since a collective may still be running).  The exchange schedule -- which record slots
+ * go through one all-reduce -- depends only on the call sequence and the group size agreed at
+ * tk_decomp_create (TKHIP_XCH_GROUP, max over the ranks), never on rank-local state; create
+ * also checks that every rank describes the same decomposition (d_total, kmax, method, n). */
+
 /* Exp-sum-term split (more ranks than factors): a rank holding a REPLICA of
  * factors another rank owns runs the same steps (bitwise the same basis) but sends zero rows
  * into the records all-reduce, so every factor's record is counted once; at convergence each

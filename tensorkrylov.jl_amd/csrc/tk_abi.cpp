@@ -12,13 +12,16 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <exception>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tk.h"
 #include "tk_internal.h"
+#include "tk_xsched.h"
 
 using namespace tk;
 
@@ -82,6 +85,9 @@ struct tk_ctx {
     long cnt[TCLS_N] = {0};
     double* xbuf = nullptr;   // host-allreduce staging
     size_t xcap = 0;
+    // a wait on the other ranks expired (TKHIP_WAIT_S): a collective may still be running on
+    // this device, so its buffers, streams and communicator are left to process exit
+    bool stuck = false;
     std::vector<hipEvent_t> evpool;   // recycled timing events (no hipEventCreate per step)
     // Handles may be destroyed in any order (Julia finalizers, Python GC): matrices and
     // decompositions hold a reference on their context, decompositions on their matrices.
@@ -137,6 +143,74 @@ static void drain_timers(tk_ctx* c) {
     }
 }
 
+// ------------------------------------------------------------------ bounded waits
+// Every wait that can depend on another rank (the records exchange, host all-reduces, a
+// stream that may sit behind a collective) has a wall-clock limit: TKHIP_WAIT_S seconds
+// (default 120).  On expiry the call returns TK_ERR_RCCL saying what it waited for, which
+// record slot and step, and RCCL's asynchronous error state -- a peer that never joins a
+// collective ends in a diagnosis, not in a job killed at its time limit.
+static double wait_limit_s() {
+    const char* e = getenv("TKHIP_WAIT_S");
+    const double v = e ? atof(e) : 120.0;
+    return v > 0 ? v : 120.0;
+}
+
+static const char* comm_state(tk_ctx* c) {
+    if (!c->comm) return "no communicator";
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(c->comm, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+    return r == ncclSuccess ? "no asynchronous error: a peer has not entered the collective" : ncclGetErrorString(r);
+}
+
+static tk_status wait_expired(tk_ctx* c, const char* what, int slot) {
+    c->stuck = true;
+    return fail(TK_ERR_RCCL, "%s: not complete after %.0f s (record slot %d = step %d; rank %d of %d; RCCL: %s)",
+                what, wait_limit_s(), slot, slot - 1, c->rank, c->nranks, comm_state(c));
+}
+
+struct Deadline {
+    typedef std::chrono::steady_clock clk;
+    clk::time_point t0 = clk::now();
+    double lim = wait_limit_s();
+    double elapsed() const { return std::chrono::duration<double>(clk::now() - t0).count(); }
+    // true once expired; backs off to short sleeps after the first millisecond
+    bool tick() {
+        const double el = elapsed();
+        if (el > lim) return true;
+        if (el > 1e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        return false;
+    }
+};
+
+// hipStreamSynchronize with a deadline
+static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int slot = -1) {
+    Deadline dl;
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return TK_OK;
+        if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+        if (dl.tick()) return wait_expired(c, what, slot);
+    }
+}
+
+// hipEventSynchronize with a deadline
+static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int slot = -1) {
+    Deadline dl;
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return TK_OK;
+        if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+        if (dl.tick()) return wait_expired(c, what, slot);
+    }
+}
+
+#define STUCKCHK(c)                                                                                   \
+    do {                                                                                              \
+        if ((c)->stuck)                                                                               \
+            return fail(TK_ERR_RCCL, "the communicator is unusable: an earlier wait on the other ranks " \
+                                     "expired (TKHIP_WAIT_S)");                                       \
+    } while (0)
+
 extern "C" {
 
 const char* tk_last_error(void) { return g_err; }
@@ -168,8 +242,9 @@ tk_status tk_ctx_create(int device, tk_ctx** out) { TK_API_BEGIN
 static void ctx_release(tk_ctx* c) {
     if (--c->refs > 0) return;
     hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
-    hipStreamSynchronize(c->xstream);
+    if (!c->stuck) sync_bounded(c, c->stream, "tk_ctx_destroy");
+    if (!c->stuck) sync_bounded(c, c->xstream, "tk_ctx_destroy");
+    if (c->stuck) return;   // a collective may still run: its resources are left to process exit
     drain_timers(c);
     for (hipEvent_t e : c->evpool) hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
@@ -189,9 +264,9 @@ tk_status tk_ctx_destroy(tk_ctx* c) { TK_API_BEGIN
 tk_status tk_ctx_sync(tk_ctx* c) { TK_API_BEGIN
     CHECKARG(c, "ctx is NULL");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipStreamSynchronize(c->xstream));
-    return TK_OK;
+    STUCKCHK(c);
+    tk_status st = sync_bounded(c, c->stream, "tk_ctx_sync (compute stream)");
+    return st ? st : sync_bounded(c, c->xstream, "tk_ctx_sync (exchange stream)");
     TK_API_END
 }
 
@@ -218,9 +293,10 @@ tk_status tk_comm_init(tk_ctx* c, const char id[128], int nranks, int rank) { TK
     TK_API_END
 }
 
-tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_BEGIN
-    CHECKARG(c && buf, "NULL argument");
-    if (!c->comm || c->nranks == 1) return TK_OK;
+// In-place all-reduce of host doubles through the device, after every records exchange
+// already enqueued (collectives keep one order on every rank); bounded waits.
+static tk_status host_allreduce(tk_ctx* c, double* buf, size_t count, ncclRedOp_t op, const char* what) {
+    STUCKCHK(c);
     HIPCHK(hipSetDevice(c->device));
     if (count > c->xcap) {
         if (c->xbuf) hipFree(c->xbuf);
@@ -228,12 +304,18 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_
         HIPCHK(hipMalloc(&c->xbuf, count * sizeof(double)));
         c->xcap = count;
     }
-    HIPCHK(hipStreamSynchronize(c->xstream));
+    tk_status st = sync_bounded(c, c->xstream, what);
+    if (st) return st;
     HIPCHK(hipMemcpyAsync(c->xbuf, buf, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    NCCLCHK(ncclAllReduce(c->xbuf, c->xbuf, count, ncclDouble, ncclSum, c->comm, c->stream));
+    NCCLCHK(ncclAllReduce(c->xbuf, c->xbuf, count, ncclDouble, op, c->comm, c->stream));
     HIPCHK(hipMemcpyAsync(buf, c->xbuf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return TK_OK;
+    return sync_bounded(c, c->stream, what);
+}
+
+tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_BEGIN
+    CHECKARG(c && buf, "NULL argument");
+    if (!c->comm || c->nranks == 1) return TK_OK;
+    return host_allreduce(c, buf, count, ncclSum, "tk_comm_allreduce_host");
     TK_API_END
 }
 
@@ -509,8 +591,8 @@ static void mat_release(tk_mat* A) {
     if (--A->refs > 0) return;
     tk_ctx* c = A->ctx;
     hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
-    free_mat(A);
+    if (!c->stuck) sync_bounded(c, c->stream, "tk_matrix_destroy");
+    if (!c->stuck) free_mat(A);   // (stuck: device buffers left to process exit)
     ctx_release(c);
 }
 
@@ -583,12 +665,18 @@ struct tk_decomp {
     // = its sequence number (host-mapped); xslot_seq[slot] = the number to wait for
     unsigned long long* xdone = nullptr;
     std::vector<unsigned long long> xslot_seq;
-    // signalled exchanges are batched: the slots of xgroup consecutive steps go through ONE
-    // all-reduce (TKHIP_XCH_GROUP, default 4); [xp0, xp1] = slots signalled but not yet
-    // exchanged, xev[slot] = the slot whose ev_x marks the exchange that carried it
-    int xgroup = 4;
-    int xp0 = -1, xp1 = -1;
+    // which slots go through which all-reduce (tk_xsched.h): the slots of xs.group
+    // consecutive steps (TKHIP_XCH_GROUP, default 4, agreed over the ranks at create) per
+    // call; xev[slot] = the slot whose ev_x marks the exchange that carried it; xcnt[slot] =
+    // the signal count (xcount) at which the slot's record is written
+    XSched xs;
     std::vector<int> xev;
+    std::vector<unsigned long long> xcnt;
+    // TKHIP_TEST_XCH_STALL=s (tests): the exchange of the range holding slot s waits on a
+    // word nobody writes until a reader's deadline expires (a peer that never joins)
+    int stall_slot = -1;
+    unsigned long long* stallw = nullptr;
+    unsigned long long stall_v = 0;
     hipStream_t cstream = nullptr;          // record copies (multi-rank): no wait on the compute queue
     int last_j = -1;
     std::vector<tk_mat*> mats;
@@ -620,6 +708,10 @@ static tk_status dalloc(tk_decomp* dc, void** p, size_t bytes) {
 }
 
 static void free_decomp(tk_decomp* dc) {
+    if (dc->ctx->stuck) {   // a collective may still read or write these buffers
+        delete dc;
+        return;
+    }
     for (hipEvent_t e : dc->ev_c) hipEventDestroy(e);
     for (hipEvent_t e : dc->ev_x) hipEventDestroy(e);
     for (void* p : dc->allocs) hipFree(p);
@@ -627,6 +719,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
     if (dc->xflag) hipFree(dc->xflag);
+    if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
     if (dc->hdone) hipHostFree(dc->hdone);
     if (dc->xdone) hipHostFree(dc->xdone);
@@ -850,10 +943,45 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
         dc->xslot_seq.assign(kmax + 2, 0);
+        dc->xcnt.assign(kmax + 2, 0);
         dc->xev.resize(kmax + 2);
         for (int i = 0; i < kmax + 2; ++i) dc->xev[i] = i;
-        if (const char* eg = getenv("TKHIP_XCH_GROUP")) dc->xgroup = std::min(64, std::max(1, atoi(eg)));
+        if (const char* eg = getenv("TKHIP_XCH_GROUP")) dc->xs.group = std::min(64, std::max(1, atoi(eg)));
+        if (const char* es = getenv("TKHIP_TEST_XCH_STALL")) {
+            void* p = nullptr;
+            if (dc->recv != dc->rec && hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p) {
+                if (hipMemcpy(&dc->stall_v, p, 8, hipMemcpyDeviceToHost) == hipSuccess) {
+                    dc->stallw = (unsigned long long*)p;
+                    dc->stall_slot = atoi(es);
+                } else {
+                    hipFree(p);
+                }
+            }
+        }
         (void)hipGetLastError();
+    }
+    if (dc->recv != dc->rec && c->nranks > 1) {
+        // preflight: every rank must describe the same decomposition, and the exchange group
+        // size is agreed (max) -- the all-reduce sequence must not depend on one rank's env
+        const char* names[5] = {"d_total", "kmax", "method", "n", "record length"};
+        double v[6] = {(double)d_total, (double)kmax, (double)method, (double)n, (double)dc->m, (double)dc->xs.group};
+        double b[12];
+        for (int i = 0; i < 6; ++i) {
+            b[i] = v[i];
+            b[6 + i] = -v[i];
+        }
+        st = host_allreduce(c, b, 12, ncclMax, "tk_decomp_create preflight");
+        if (st) {
+            free_decomp(dc);
+            return st;
+        }
+        for (int i = 0; i < 5; ++i)
+            if (b[i] != -b[6 + i]) {
+                free_decomp(dc);
+                return fail(TK_ERR_ARG, "tk_decomp_create: the %d ranks disagree on %s (min %.17g, max %.17g)",
+                            c->nranks, names[i], -b[6 + i], b[i]);
+            }
+        dc->xs.group = (int)b[5];
     }
     c->refs++;
     for (tk_mat* A : dc->mats) A->refs++;
@@ -863,6 +991,8 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
 }
 
 int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
+
+int tk_decomp_next_step(tk_decomp* dc) { return dc ? dc->jnext : -1; }
 
 tk_status tk_decomp_set_replica(tk_decomp* dc, int replica) { TK_API_BEGIN
     CHECKARG(dc, "NULL handle");
@@ -888,20 +1018,29 @@ int tk_decomp_arnoldi_sweeps(tk_decomp* dc) {
     return dc->onesweep ? 1 : 2;
 }
 
-static tk_status exchange_pending(tk_decomp* dc);
-static tk_status bk_flush(tk_decomp* dc, double* rec_out = nullptr);
+tk_status tk_decomp_agree(tk_decomp* dc, int* vals, int count) { TK_API_BEGIN
+    CHECKARG(dc && (vals || count == 0) && count >= 0 && count <= 64, "bad argument");
+    tk_ctx* c = dc->ctx;
+    if (dc->recv == dc->rec || c->nranks == 1 || count == 0) return TK_OK;
+    double b[64];
+    for (int i = 0; i < count; ++i) b[i] = vals[i];
+    tk_status st = host_allreduce(c, b, count, ncclMax, "tk_decomp_agree");
+    if (st) return st;
+    for (int i = 0; i < count; ++i) vals[i] = (int)b[i];
+    return TK_OK;
+    TK_API_END
+}
 
 tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     if (!dc) return TK_OK;
     tk_ctx* c = dc->ctx;
     std::vector<tk_mat*> mats = dc->mats;
     hipSetDevice(c->device);
-    if (!dc->failed) {   // (records of slots nobody will read: harmless)
-        bk_flush(dc);
-        exchange_pending(dc);
-    }
-    hipStreamSynchronize(c->stream);
-    hipStreamSynchronize(c->xstream);
+    // No collective starts here (a peer whose step failed never joins it): slots whose
+    // group never filled are dropped -- nobody reads them.  Already enqueued exchanges are
+    // waited for with the deadline.
+    if (!c->stuck) sync_bounded(c, c->stream, "tk_decomp_destroy (compute stream)");
+    if (!c->stuck) sync_bounded(c, c->xstream, "tk_decomp_destroy (exchange stream)");
     free_decomp(dc);
     for (tk_mat* A : mats) mat_release(A);
     ctx_release(c);
@@ -940,24 +1079,30 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     return a;
 }
 
-// One RCCL all-reduce per group of record slots: the send buffer holds only this rank's
+// One RCCL all-reduce per range of record slots: the send buffer holds only this rank's
 // rows (other rows stay zero forever), so the sum is exact and every rank receives every
-// factor's record.  Slots [s0, s1] are contiguous in memory, so a group is one call.
-static tk_status exchange_range(tk_decomp* dc, int s0, int s1, bool signalled) {
+// factor's record.  Slots [s0, s1] are contiguous in memory, so a range is one call.
+// Which ranges go out when is decided by dc->xs (tk_xsched.h), identically on every rank.
+static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
     tk_ctx* c = dc->ctx;
+    STUCKCHK(c);
     const size_t cnt = (size_t)dc->d_total * dc->m;
     double* s = (dc->zrec ? dc->zrec : dc->rec) + (size_t)s0 * cnt;
     double* r = dc->recv + (size_t)s0 * cnt;
     const size_t tot = cnt * (size_t)(s1 - s0 + 1);
-    // the exchange runs on its own stream, overlapping the next steps' kernels; it starts
-    // when the steps' k_post blocks have signalled (or after an event marker)
-    if (signalled) {
-        HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcount, hipStreamWaitValueGte,
+    // the exchange runs on its own stream, overlapping the next steps' kernels.  Step slots
+    // start when the steps' k_post blocks have signalled (the count at which slot s1 was
+    // written); init / flush slots and handles without the signal word after an event marker
+    if (dc->xflag && s0 >= 1 && s1 <= dc->kmax) {
+        HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcnt[s1], hipStreamWaitValueGte,
                                     0xFFFFFFFFFFFFFFFFull));
     } else {
         HIPCHK(hipEventRecord(dc->ev_c[s1], c->stream));
         HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[s1], 0));
     }
+    if (dc->stallw && dc->stall_slot >= s0 && dc->stall_slot <= s1)
+        HIPCHK(hipStreamWaitValue64(c->xstream, dc->stallw, dc->stall_v + 1, hipStreamWaitValueGte,
+                                    0xFFFFFFFFFFFFFFFFull));
     {
         Timer tm(c, TCLS_XCH, 2, c->xstream);
         NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
@@ -974,44 +1119,27 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1, bool signalled) {
     return TK_OK;
 }
 
-// Enqueue the exchange of the signalled slots still waiting for their group to fill.
-static tk_status exchange_pending(tk_decomp* dc) {
-    if (dc->xp0 < 0) return TK_OK;
-    const int s0 = dc->xp0, s1 = dc->xp1;
-    dc->xp0 = dc->xp1 = -1;
-    return exchange_range(dc, s0, s1, true);
+static tk_status xsend(tk_decomp* dc, XSched::Range r) {
+    if (r.first > r.second) return TK_OK;
+    for (int s = r.first; s <= r.second; ++s)
+        if (!dc->xs.written(s))
+            return fail(TK_ERR_STATE, "records exchange: slot %d (step %d) is not written on this rank", s, s - 1);
+    return exchange_range(dc, r.first, r.second);
 }
 
-static tk_status exchange_and_copy(tk_decomp* dc, int slot, double* rec_out, bool signalled = false) {
+// Copy one slot's (all-reduced, on several ranks) records to the host.
+static tk_status copy_slot(tk_decomp* dc, int slot, double* rec_out) {
+    if (!rec_out) return TK_OK;
     tk_ctx* c = dc->ctx;
     const size_t cnt = (size_t)dc->d_total * dc->m;
-    double* r = dc->recv + (size_t)slot * cnt;
     if (dc->recv != dc->rec) {
-        if (signalled && !rec_out && dc->xgroup > 1) {
-            // batched: the slot joins the pending group; a full group goes out as one call
-            if (dc->xp0 >= 0 && slot != dc->xp1 + 1) {
-                tk_status st = exchange_pending(dc);
-                if (st) return st;
-            }
-            if (dc->xp0 < 0) dc->xp0 = slot;
-            dc->xp1 = slot;
-            return dc->xp1 - dc->xp0 + 1 >= dc->xgroup ? exchange_pending(dc) : TK_OK;
-        }
-        // exchanges run in slot order: what is pending goes first
-        tk_status st = exchange_pending(dc);
-        if (st) return st;
-        st = exchange_range(dc, slot, slot, signalled);
-        if (st) return st;
-        if (rec_out) {
-            HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->xstream));
-            HIPCHK(hipStreamSynchronize(c->xstream));
-        }
-        return TK_OK;
+        HIPCHK(hipMemcpyAsync(rec_out, dc->recv + (size_t)slot * cnt, cnt * sizeof(double), hipMemcpyDeviceToHost,
+                              c->xstream));
+        return sync_bounded(c, c->xstream, "records exchange", slot);
     }
-    if (rec_out) {
-        HIPCHK(hipMemcpyAsync(rec_out, r, cnt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-    }
+    HIPCHK(hipMemcpyAsync(rec_out, dc->rec + (size_t)slot * cnt, cnt * sizeof(double), hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return TK_OK;
 }
 
@@ -1028,17 +1156,17 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
     } while (0);                           \
     LAUNCHCHK(name)
 
-// Step j's record is enqueued (its k_post, or the bookkeeping block of the next k_arn_d1):
-// count its signal, note its host sequence number, and exchange its slot.
-static tk_status complete_step(tk_decomp* dc, int j, unsigned long long seqj, double* rec_out) {
-    const bool sig = dc->xflag != nullptr;
-    if (sig) dc->xcount += (unsigned long long)dc->nf;   // one add per factor
+// Step j's record is enqueued on this rank (its k_post, or the bookkeeping block of the
+// next k_arn_d1): count its signal and note its host sequence number.  Local only.
+static void complete_step(tk_decomp* dc, int j, unsigned long long seqj) {
+    if (dc->xflag) dc->xcount += (unsigned long long)dc->nf;   // one add per factor
     if (dc->hdone) dc->slot_seq[j + 1] = seqj;
-    return exchange_and_copy(dc, j + 1, rec_out, sig);
+    dc->xcnt[j + 1] = dc->xcount;
+    dc->xs.complete(j + 1);
 }
 
-// The deferred bookkeeping of the last one-sweep step as a k_post of its own.
-static tk_status bk_flush(tk_decomp* dc, double* rec_out) {
+// The deferred bookkeeping of the last one-sweep step as a k_post of its own.  Local only.
+static tk_status bk_flush(tk_decomp* dc) {
     if (dc->bk_j < 0) return TK_OK;
     tk_ctx* c = dc->ctx;
     hipStream_t s = c->stream;
@@ -1046,9 +1174,19 @@ static tk_status bk_flush(tk_decomp* dc, double* rec_out) {
     const KArgs ax = dc->bk_args;
     dc->bk_j = -1;
     RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, ax, POST_ARN_D, 0, 1, s), "post");
-    return complete_step(dc, j, ax.seq, rec_out);
+    complete_step(dc, j, ax.seq);
+    return TK_OK;
 }
 
+// Multi-rank: slots <= S exchanged now (the deferred bookkeeping of the last step first).
+static tk_status need_slots(tk_decomp* dc, int S) {
+    if (dc->recv == dc->rec || S <= dc->xs.sent) return TK_OK;
+    if (dc->bk_j >= 0 && dc->bk_j + 1 <= S) {
+        tk_status st = bk_flush(dc);
+        if (st) return st;
+    }
+    return xsend(dc, dc->xs.need(S));
+}
 
 tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     CHECKARG(dc, "NULL decomp");
@@ -1078,7 +1216,15 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     dc->jnext = 0;
     dc->pending = false;
     dc->last_j = -1;
-    return exchange_and_copy(dc, 0, rec_out);
+    // a new sequence: slots of the previous one that never went out are dropped (on every rank)
+    dc->xs.reset();
+    dc->xcnt[0] = dc->xcount;
+    dc->xs.complete(0);
+    if (dc->recv != dc->rec) {
+        st = xsend(dc, dc->xs.need(0));
+        if (st) return st;
+    }
+    return copy_slot(dc, 0, rec_out);
     TK_API_END
 }
 
@@ -1267,13 +1413,26 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     if (dc->bk_j == j) {
         // one sweep: this launch carried step j-1's bookkeeping (its record is complete);
         // step j's own waits for the next launch unless the caller wants it now
-        if (prev_bk == j - 1 && prev_bk >= 0) {
-            st = complete_step(dc, prev_bk, prev_seq, nullptr);
+        if (prev_bk == j - 1 && prev_bk >= 0) complete_step(dc, prev_bk, prev_seq);
+        if (rec_out || !dc->bk_fold) {
+            st = bk_flush(dc);
             if (st) return st;
         }
-        return rec_out || !dc->bk_fold ? bk_flush(dc, rec_out) : TK_OK;
+    } else {
+        complete_step(dc, j, dc->seq);
     }
-    return complete_step(dc, j, dc->seq, rec_out);
+    if (dc->recv != dc->rec) {
+        // canonical: slots <= j are written on every rank now; full groups go out
+        for (const XSched::Range& r : dc->xs.step_done(j)) {
+            st = xsend(dc, r);
+            if (st) return st;
+        }
+        if (rec_out) {
+            st = need_slots(dc, j + 1);
+            if (st) return st;
+        }
+    }
+    return copy_slot(dc, j + 1, rec_out);
     TK_API_END
 }
 
@@ -1287,7 +1446,7 @@ tk_status tk_decomp_sweep(tk_decomp* dc, int j0, int j1) { TK_API_BEGIN
     for (int j = j0; j < j1 && st == TK_OK; ++j) st = tk_decomp_step(dc, j, nullptr);
     dc->in_sweep = false;
     if (st == TK_OK) st = bk_flush(dc);
-    if (st == TK_OK) st = exchange_pending(dc);
+    if (st == TK_OK) st = need_slots(dc, dc->jnext);
     return st;
     TK_API_END
 }
@@ -1298,14 +1457,17 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     HIPCHK(hipSetDevice(dc->ctx->device));
     {
         tk_status st0 = bk_flush(dc);
+        if (st0 == TK_OK) st0 = need_slots(dc, dc->jnext);   // every issued step's slot first
         if (st0) return st0;
     }
     const int slot = dc->kmax + 1;
+    const bool multi = dc->recv != dc->rec;
     if (!dc->pending) {
         if (rec_out) {
             tk_status st = clear_slot(dc, slot);
+            if (st == TK_OK && multi) st = exchange_range(dc, slot, slot);
             if (st) return st;
-            return exchange_and_copy(dc, slot, rec_out);
+            return copy_slot(dc, slot, rec_out);
         }
         return TK_OK;
     }
@@ -1315,22 +1477,37 @@ tk_status tk_decomp_flush(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     st = finalize_pending(dc, a);
     if (st) return st;
     dc->pending = false;
-    return exchange_and_copy(dc, slot, rec_out);
+    if (multi) {
+        st = exchange_range(dc, slot, slot);
+        if (st) return st;
+    }
+    return copy_slot(dc, slot, rec_out);
     TK_API_END
+}
+
+// TKHIP_TEST_XCH_STALL: release the exchange stream held at the stalled range (tests)
+static void release_stall(tk_decomp* dc) {
+    if (!dc->stallw) return;
+    const unsigned long long v = dc->stall_v + 1;
+    hipMemcpy(dc->stallw, &v, sizeof v, hipMemcpyHostToDevice);
 }
 
 tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API_BEGIN
     CHECKARG(dc && out, "NULL argument");
     CHECKARG(s0 >= 0 && s1 <= dc->kmax + 2 && s0 <= s1, "slot range");
-    HIPCHK(hipSetDevice(dc->ctx->device));
+    tk_ctx* c = dc->ctx;
+    HIPCHK(hipSetDevice(c->device));
     const size_t per = (size_t)dc->d_total * dc->m;
     if (s1 == s0) return TK_OK;
-    if (dc->bk_j >= 0 && dc->bk_j + 1 >= s0 && dc->bk_j + 1 < s1 && !dc->failed) {
+    if (dc->recv != dc->rec) {
+        // the step slots up to s1-1 go out now if their group has not (the flush slot went
+        // out with its flush); canonical on every rank
+        if (!dc->failed) {
+            tk_status st = need_slots(dc, std::min(s1 - 1, dc->jnext));
+            if (st) return st;
+        }
+    } else if (dc->bk_j >= 0 && dc->bk_j + 1 >= s0 && dc->bk_j + 1 < s1 && !dc->failed) {
         tk_status st = bk_flush(dc);
-        if (st) return st;
-    }
-    if (dc->xp0 >= 0 && s1 - 1 >= dc->xp0) {
-        tk_status st = exchange_pending(dc);
         if (st) return st;
     }
     bool hosted = dc->hdone != nullptr;
@@ -1338,6 +1515,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     if (hosted) {
         // wait for the steps that wrote these slots only (later steps may be queued or
         // running), then read their records from host-mapped memory
+        Deadline dl;
         for (int sl = s0; sl < s1; ++sl) {
             const unsigned long long want = dc->slot_seq[sl];
             const unsigned long long* w = dc->hdone + (size_t)sl * dc->nf;
@@ -1346,11 +1524,13 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
                 while (__atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want) {
                     if (++spins % 4096 == 0) {
                         // the device may have failed: surface its error instead of spinning
-                        hipError_t e = hipStreamQuery(dc->ctx->stream);
+                        hipError_t e = hipStreamQuery(c->stream);
                         if (e != hipSuccess && e != hipErrorNotReady)
                             return fail(TK_ERR_HIP, "waiting for step records: %s", hipGetErrorString(e));
                         if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)
                             return fail(TK_ERR_STATE, "step records of slot %d never arrived", sl);
+                        if (dl.elapsed() > dl.lim)
+                            return fail(TK_ERR_HIP, "step records of slot %d: not complete after %.0f s", sl, dl.lim);
                     }
                 }
             }
@@ -1362,16 +1542,22 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     for (int sl = s0; sl < s1 && xhosted; ++sl) xhosted = dc->xslot_seq[sl] != 0;
     if (xhosted) {
         // multi-rank: wait for the exchange stream's mirror of each slot (host-mapped words)
+        Deadline dl;
         for (int sl = s0; sl < s1; ++sl) {
             const unsigned long long want = dc->xslot_seq[sl];
             long spins = 0;
             while (__atomic_load_n(dc->xdone + sl, __ATOMIC_ACQUIRE) < want) {
                 if (++spins % 4096 == 0) {
-                    hipError_t e = hipStreamQuery(dc->ctx->xstream);
+                    hipError_t e = hipStreamQuery(c->xstream);
                     if (e != hipSuccess && e != hipErrorNotReady)
                         return fail(TK_ERR_HIP, "waiting for exchanged records: %s", hipGetErrorString(e));
                     if (e == hipSuccess && __atomic_load_n(dc->xdone + sl, __ATOMIC_ACQUIRE) < want)
                         return fail(TK_ERR_STATE, "exchanged records of slot %d never arrived", sl);
+                    if (dl.elapsed() > dl.lim) {
+                        const tk_status st = wait_expired(c, "records exchange", sl);
+                        release_stall(dc);
+                        return st;
+                    }
                 }
             }
         }
@@ -1381,16 +1567,23 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     if (dc->cstream && dc->recv != dc->rec) {
         // multi-rank: the slots are final once the exchange of the last one has run
         // (exchanges run in slot order on the exchange stream); copy on a stream of its own
-        HIPCHK(hipEventSynchronize(dc->ev_x[dc->xev[s1 - 1]]));
+        tk_status st = event_bounded(c, dc->ev_x[dc->xev[s1 - 1]], "records exchange", s1 - 1);
+        if (st) {
+            release_stall(dc);
+            return st;
+        }
         HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                               dc->cstream));
         HIPCHK(hipStreamSynchronize(dc->cstream));
         return TK_OK;
     }
-    HIPCHK(hipStreamSynchronize(dc->ctx->xstream));
+    if (dc->recv != dc->rec) {
+        tk_status st = sync_bounded(c, c->xstream, "records exchange", s1 - 1);
+        if (st) return st;
+    }
     HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
-                          dc->ctx->stream));
-    HIPCHK(hipStreamSynchronize(dc->ctx->stream));
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return TK_OK;
     TK_API_END
 }
@@ -1436,6 +1629,7 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
     if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
     {
         tk_status st0 = bk_flush(dc);
+        if (st0 == TK_OK && dc->pending) st0 = need_slots(dc, dc->jnext);   // as tk_decomp_flush
         if (st0) return st0;
     }
     // a pending column is finalized first; for Arnoldi with the one-tile flush kernel it is
@@ -1495,8 +1689,10 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
             RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, a, POST_ARN_FIN, 0, 1, s), "post");
         }
         dc->pending = false;
-        st = exchange_and_copy(dc, slot, nullptr);
-        if (st) return st;
+        if (dc->recv != dc->rec) {
+            st = exchange_range(dc, slot, slot);
+            if (st) return st;
+        }
     } else {
         KArgs a = base_args(dc, 0, 0);
         RUN(TCLS_VY, 1, launch_basis_mul(dc->df, dc->nf, a, dc->Ydev, dc->Xdev, k, t, s), "basis_mul");

@@ -292,8 +292,15 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             klast = k - 1;
             break;
         }
-    const int P = std::max(1, std::min(nthreads, 64));
-    depth = std::max(depth, P + 1);
+    // every rank must issue the same sequence of steps and record reads (the records
+    // all-reduces follow it, tk_xsched.h): agree the worker count and depth (max over ranks)
+    int agreed[2] = {std::max(1, std::min(nthreads, 64)), depth};
+    {
+        tk_status st0 = tk_decomp_agree(dc, agreed, 2);
+        if (st0) return st0;
+    }
+    const int P = agreed[0];
+    depth = std::max(agreed[1], P + 1);
     *outcome = 0;
     *k_end = klast;
     std::vector<double> rec((size_t)sv->d * sv->m);

@@ -15,5 +15,6 @@ from .decompositions import (METHODS, Decomposition, Partition, TensorArnoldi,  
 from .device import Context, DeviceDecomposition, DeviceMatrix, unique_id  # noqa: F401
 from .solver import solve_tensorized_system, tensorkrylov  # noqa: F401
 from .structures import (ConvDiff, ConvergenceData, KroneckerMatrix, KruskalTensor,  # noqa: F401
+                         kronecker_sum_matvec, kroneckervectorize,
                          Laplace, NonSymInstance, RandSparseSPD, SymInstance, TensorizedSystem,
                          as_csc, assemble_matrix, normalize_rhs, random_rhs)

@@ -149,6 +149,10 @@ class TensorDecomposition:
         host's compressed solve of step k-1).  Columns <= k-1 of V, H and b~ are not
         touched by step k, so results are the same as with orthonormalize(k)."""
         j = k - 1
+        if j < getattr(self.dev, "next_step", 0):
+            # already enqueued (the native loop, tk_solver_run, issues steps ahead of the
+            # records it reads): its record waits on the device for collect()
+            return
         if hasattr(self.dev, "step_async"):
             self.dev.step_async(j)
         else:

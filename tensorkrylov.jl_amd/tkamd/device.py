@@ -139,6 +139,12 @@ class DeviceDecomposition:
         """Records exchange triggered by a signal word, not an event (tk_decomp_exchange_signalled)."""
         return bool(self.ctx._lib.tk_decomp_exchange_signalled(self.h))
 
+    @property
+    def next_step(self):
+        """The next step index the device accepts (tk_decomp_next_step): steps below it are
+        enqueued, possibly by a driver that ran ahead of the records read so far."""
+        return int(self.ctx._lib.tk_decomp_next_step(self.h))
+
     def set_replica(self, on=True):
         """This rank's factors are replicas of another rank's (tk_decomp_set_replica): same
         steps, zero rows sent into the records all-reduce."""

@@ -174,6 +174,52 @@ class KruskalTensor:
     def ndims(self):
         return len(self.fmat)
 
+    def size(self):
+        """Base.size (src/tensor_struct.jl:323): the row count of every factor matrix."""
+        return tuple(int(np.asarray(F).shape[0]) for F in self.fmat)
+
+    def redistribute(self, mode):
+        """redistribute!(x, mode) (src/tensor_struct.jl:325-333): column j of factor `mode`
+        (0-based here) scaled by lambda[j], in place (lambda itself is left as it is)."""
+        F = np.array(self.fmat[mode], dtype=np.float64)
+        for j in range(self.ncomponents()):
+            F[:, j] = self.lam[j] * F[:, j]
+        self.fmat[mode] = F
+
+
+def kroneckervectorize(x):
+    """kroneckervectorize(x) (src/tensor_struct.jl:361-384): the length prod(size(x))
+    vector sum_i x_d[:, i] kron ... kron (lambda_i x_1[:, i]) -- vec of the Kruskal tensor with
+    the first mode running fastest.  Like the reference it first calls redistribute!(x, 1),
+    so x's first factor is left scaled by lambda (call it once per tensor)."""
+    x.redistribute(0)
+    N = int(np.prod(x.size()))
+    vecx = np.zeros(N)
+    for i in range(x.ncomponents()):
+        tmp = np.asarray(x.fmat[-1])[:, i]
+        for j in range(x.ndims() - 2, -1, -1):
+            tmp = np.kron(tmp, np.asarray(x.fmat[j])[:, i])
+        vecx += tmp
+    return vecx
+
+
+def kronecker_sum_matvec(A, v):
+    """(sum_s I kron .. kron A_s kron .. kron I) v for the Kronecker-sum operator of
+    KroneckerMatrix A (the system the reference solves, src/system.jl:15-43), with v in
+    kroneckervectorize's ordering: A_s acts on mode s, mode 1 fastest.  Small sizes only
+    (test use: the explicit residual of a solution)."""
+    import scipy.sparse as sp
+    dims = A.dimensions()
+    X = np.asarray(v, dtype=np.float64).reshape(dims[::-1])   # axes (d, ..., 1): mode s on axis d-1-s
+    out = np.zeros_like(X)
+    for s in range(len(dims)):
+        colptr, rowval, nzval = A[s]
+        M = sp.csc_matrix((nzval, rowval, colptr), shape=(dims[s], dims[s]))
+        ax = len(dims) - 1 - s
+        Xs = np.moveaxis(X, ax, 0).reshape(dims[s], -1)
+        out += np.moveaxis((M @ Xs).reshape(np.moveaxis(X, ax, 0).shape), 0, ax)
+    return out.ravel()
+
 
 def random_rhs(d, n, rng=None):
     """random_rhs (src/system.jl:5-11): ONE rand(n) vector shared by all d slots."""

@@ -195,3 +195,39 @@ def test_replica_sends_zero_rows_and_splits_terms(ctx, method, monkeypatch):
         ref = Xo[f][:, c0:c1]
         assert Xr[f].shape == ref.shape and empty[f].shape == (n, 0)
         assert np.abs(Xr[f] - ref).max() <= 1e-14 * np.abs(ref).max()
+
+
+def test_exchange_wait_has_a_deadline(monkeypatch):
+    """A records exchange that never completes (TKHIP_TEST_XCH_STALL: the all-reduce of the
+    group holding slot 7 (slots 5..8) waits on a word nobody writes -- a peer that never joins) ends in
+    TK_ERR_RCCL after TKHIP_WAIT_S, naming the slot / step and RCCL's state, instead of
+    spinning forever; afterwards the communicator refuses further collectives at once and
+    destroy returns (its buffers are left to process exit).  1-rank communicator."""
+    import time
+    tk = _tk()
+    n, K, d = 3000, 12, 2
+    csc = tk.assemble_matrix(n, "Laplace")
+    rng = np.random.default_rng(11)
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    c = tk.Context(0)
+    c.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_TEST_XCH_STALL", "7")
+    monkeypatch.setenv("TKHIP_WAIT_S", "2")
+    A = tk.DeviceMatrix(c, csc)
+    dev = tk.DeviceDecomposition(c, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+    dev.init(False)
+    dev.sweep(0, K)                             # enqueues without waiting
+    r1 = dev.records(1, 5)                      # slots 1..4 went out before the stalled group
+    assert r1.shape == (4, d, dev.m) and (r1[:, :, dev.layout.beta] > 0).all()
+    t0 = time.time()
+    with pytest.raises(tk.TKError, match=r"error 5: records exchange: not complete after 2 s \(record slot 7 = step 6"):
+        dev.records(7, 8)
+    assert time.time() - t0 < 30
+    with pytest.raises(tk.TKError, match="communicator is unusable"):
+        dev.flush()
+    t0 = time.time()
+    dev.close()
+    A.close()
+    c.close()
+    assert time.time() - t0 < 30

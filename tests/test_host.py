@@ -390,3 +390,60 @@ def test_native_residual_breakdown_status():
                              ctypes.c_double(10.0), ctypes.byref(rc), ctypes.byref(rn))
     assert st == L.TK_BREAKDOWN and rc.value < 0
     assert lib.tk_residualnorm(0, k, t, None, None, None, None, None, 1.0, None, None) == 1   # TK_ERR_ARG
+
+
+def test_kroneckervectorize_and_kronecker_sum():
+    """kroneckervectorize (src/tensor_struct.jl:361-384): vec of the Kruskal tensor, mode 1
+    fastest, with redistribute!(x, 1) applied to x first; the Kronecker-sum operator
+    (sum_s I kron .. A_s .. kron I) against explicit kron products."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(1)
+    dims, t = (4, 3, 5), 2
+    F = [rng.standard_normal((n, t)) for n in dims]
+    lam = rng.standard_normal(t)
+    x = tkamd.KruskalTensor(lam, [f.copy() for f in F])
+    assert x.size() == dims
+    v = tkamd.kroneckervectorize(x)
+    T = np.einsum("r,ir,jr,kr->ijk", lam, *F)
+    assert np.abs(v - T.ravel(order="F")).max() <= 1e-14
+    assert np.allclose(x.fmat[0], F[0] * lam)            # redistribute!(x, 1) happened
+    csc = [tkamd.assemble_matrix(n, "ConvDiff") for n in dims]
+    A = tkamd.KroneckerMatrix(tkamd.NonSymInstance, csc, tkamd.ConvDiff)
+    M = [sp.csc_matrix((c[2], c[1], c[0]), shape=(n, n)).toarray() for c, n in zip(csc, dims)]
+    I3 = [np.eye(n) for n in dims]
+    K = (np.kron(np.kron(I3[2], I3[1]), M[0]) + np.kron(np.kron(I3[2], M[1]), I3[0])
+         + np.kron(np.kron(M[2], I3[1]), I3[0]))
+    assert np.abs(K @ v - tkamd.kronecker_sum_matvec(A, v)).max() <= 1e-14 * np.abs(K @ v).max()
+
+
+@pytest.mark.parametrize("cls,method,tol", [("Laplace", "TensorLanczos", 1e-2), ("ConvDiff", "TensorArnoldi", 0.3)])
+def test_solution_host_logic(cls, method, tol):
+    """The driver's solution output over the CPU stand-in device: the returned KruskalTensor
+    equals the oracle's x, vec(x) solves the Kronecker-sum system to the reported relative
+    residual, and X is sized by ncomponents(y) = 2r+1 for ConvDiff (SURVEY.md 3.2 deviation)."""
+    from _fake_device import backend
+    d, n = 3, 30
+    sym = cls == "Laplace"
+    if sym:
+        xs = np.arange(1, n + 1) / (n + 1)
+        b = O.normalize_rhs([xs * (1 - xs) + 0.01 * np.random.default_rng(7).random(n)] * d)
+    else:
+        b = O.normalize_rhs([np.random.default_rng(12345).random(n)] * d)
+    A = tkamd.KroneckerMatrix.gallery(tkamd.SymInstance if sym else tkamd.NonSymInstance, d, n, cls)
+    conv = tkamd.ConvergenceData(n - 1)
+    x = tkamd.tensorkrylov(conv, A, [bs.copy() for bs in b], tol, n - 1, method, backend=backend)
+    conv_o, x_o, _ = O.tensorkrylov([O.gallery_csc(n, cls)] * d, b, tol, n - 1, method, cls, sym,
+                                    A_dense=None if sym else O.convdiff_dense(n))
+    assert x is not None and x_o is not None
+    assert np.abs(x.lam - x_o[0]).max() <= 1e-12 * np.abs(x_o[0]).max()
+    for s in range(d):
+        assert np.abs(x.fmat[s] - x_o[1][s]).max() <= 1e-12 * np.abs(x_o[1][s]).max()
+    if not sym:
+        assert x.ncomponents() == 3                      # 2r+1 with r = 1
+    k = conv.niterations if conv.relative_residual_norm[-1] < tol else \
+        [i + 1 for i, r in enumerate(conv.relative_residual_norm) if i > 0 and r < tol][0]
+    vecb = b[-1]
+    for s in range(d - 2, -1, -1):
+        vecb = np.kron(vecb, b[s])
+    res = np.linalg.norm(tkamd.kronecker_sum_matvec(A, tkamd.kroneckervectorize(x)) - vecb)
+    assert abs(res - conv.relative_residual_norm[k - 1]) <= 1e-6 * conv.relative_residual_norm[k - 1]
