@@ -50,26 +50,36 @@ CONFIGS = {
 }
 
 
-def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None):
+def matrix_bytes(n, nnz, method="TensorArnoldi", sweeps=2, mat_bytes=None):
+    """Bytes of A_s one SpMV reads (SURVEY.md 8d, int32 CSR: 12 nnz + 4 (n+1)); the one-sweep
+    kernels read only what their banded storage holds (`mat_bytes`: 0 for a Toeplitz band,
+    whose diagonals are 4 scalars)."""
+    if sweeps == 1 and method in ("TensorArnoldi", "TensorLanczos") and mat_bytes is not None:
+        return mat_bytes
+    return 12 * nnz + 4 * (n + 1)
+
+
+def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None, with_matrix=True):
     """algorithmic bytes of one factor-step with k basis columns (int32 CSR).
     Arnoldi as two-sweep CGS2 (sweeps=2): B_spmv + 2 MGS passes + write V_{k+1} + the RHS
     dot.  One-sweep Arnoldi (sweeps=1, delayed reorthogonalization):
     V_1..V_{k-1} read once + the raw vector u read and written + V_k written (both SpMVs
     take their vector from LDS; <V_k, b> = norm(b) <V_k, V_1> needs no read of b) + the
-    matrix bytes its storage must read
-    (`mat_bytes`: 0 for a Toeplitz band, whose diagonals are 4 scalars).  Lanczos: B_spmv +
-    read V_{k-1} + write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new
-    column, 8n(k+1) (its redo steps are extra work, not counted)."""
-    b_spmv = 12 * nnz + 4 * (n + 1) + 8 * n + 8 * n
+    matrix bytes its storage must read (matrix_bytes).  Lanczos: B_spmv + read V_{k-1} +
+    write V_{k+1} + the RHS dot; LanczosReorth adds the Gram row of the new column, 8n(k+1)
+    (its redo steps are extra work, not counted).  with_matrix=False leaves out A_s's bytes
+    (8d: factors sharing A_s in one batched SpMV count them once per batch)."""
+    mb = matrix_bytes(n, nnz, method, sweeps, mat_bytes) if with_matrix else 0
+    vec = 8 * n + 8 * n                      # SpMV x read, y written
     if method == "TensorArnoldi" and sweeps == 1:
-        return 8 * n * (k - 1) + 3 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
+        return 8 * n * (k - 1) + 3 * 8 * n + mb
     if method == "TensorArnoldi":
-        return b_spmv + 2 * 8 * n * k + 8 * n + 8 * n
+        return mb + vec + 2 * 8 * n * k + 8 * n + 8 * n
     if method == "TensorLanczos" and sweeps == 1:
         # one-sweep TTR (k_lan_1s): u_{k-1} and v_{k-1} read, v_k and u_k written, <v_k, b>;
         # the SpMV takes v_k from LDS (+ the tracked factor's Gram row, gram_bytes_step)
-        return 5 * 8 * n + (12 * nnz + 4 * (n + 1) if mat_bytes is None else mat_bytes)
-    b = b_spmv + 8 * n + 8 * n + 8 * n
+        return 5 * 8 * n + mb
+    b = mb + vec + 8 * n + 8 * n + 8 * n
     if method == "TensorLanczosReorth":
         b += 8 * n * (k + 1)
     return b
@@ -164,6 +174,9 @@ def main():
                                      "steps": args.steps, "warmup": args.warmup})
 
     host_issue = [0.0, 0]
+    # orthogonality_data of factor 1 (src/tensor_krylov_method.jl:103): a Gram row per step,
+    # or (deferred) one MFMA SYRK of its basis per solve, timed inside the step here
+    gram_owner = dev.gram_deferred and part.first == 0 and part.nf > 0 and not part.replica
 
     def sweep():
         dev.init(False)
@@ -172,6 +185,8 @@ def main():
         host_issue[0] += time.perf_counter() - h0
         host_issue[1] += 1
         dev.basis_mul(K, Ys, want=False)   # finalizes the pending column V[:, K] first (fused for Arnoldi)
+        if gram_owner:
+            dev.gram(0, K, want=False)      # orthogonality_data for k = 2..K from one Gram
 
     def barrier():
         ctx.sync()
@@ -201,6 +216,7 @@ def main():
     sweep_ms, sweep_cnt = ctx.timing_read(L.T_SWEEP)    # K step groups per sweep
     step_ms, step_cnt = sweep_ms, sweep_cnt * K
     vy_ms, vy_cnt = ctx.timing_read(L.T_VY)
+    gram_ms, gram_cnt = ctx.timing_read(L.T_GRAM)
     if world > 1:                               # max over ranks (one-hot sum)
         v = np.zeros(world)
         v[rank] = elapsed
@@ -280,9 +296,13 @@ def main():
     iters = K * args.steps
     value = iters / elapsed
     # roofline of the Arnoldi step (SpMV + MGS2 + reductions), device time from events
-    alg_step = sum(alg_bytes_step(n, nnz, k, method, sweeps, toeplitz_bytes(csc))
-                   for k in range(1, K + 1)) * part.nf
-    if method == "TensorLanczos" and sweeps == 1 and part.first == 0:
+    # A_s's bytes once per batch of factors that share one SpMV pass over it,
+    # else once per factor (dev.matrix_reads)
+    tb = toeplitz_bytes(csc)
+    mreads = dev.matrix_reads
+    alg_step = sum(alg_bytes_step(n, nnz, k, method, sweeps, tb, with_matrix=False) * part.nf
+                   + matrix_bytes(n, nnz, method, sweeps, tb) * mreads for k in range(1, K + 1))
+    if method == "TensorLanczos" and sweeps == 1 and part.first == 0 and not dev.gram_deferred:
         # the Gram row of factor 1's new column (orthogonality_loss, src/tensor_krylov_method.jl
         # :103): its basis row is streamed for it alone
         alg_step += sum(8 * n * (k - 1) for k in range(1, K + 1))
@@ -348,6 +368,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": alg_step / K,
+                "matrix_reads_per_step": mreads,
                 "arnoldi_sweeps_over_V": sweeps if method == "TensorArnoldi" else None,
                 **({"reference_algorithm_bytes_per_launch": ref_step / K,
                     "reference_algorithm_effective_GBs": round((ref_step / K) / step_avg_s / 1e9, 1)}
@@ -361,6 +382,14 @@ def main():
                            "one read of V" if fused_vy else "k_basis_mul (MFMA) after the flush"),
                 "avg_us": round(vy_s * 1e6, 2),
             },
+            "orthogonality_gram": ({"mode": "deferred: one v_mfma_f64_16x16x4f64 SYRK of factor 1's basis "
+                                            "per solve (tk_decomp_gram)",
+                                    "avg_us": round(1e3 * gram_ms / gram_cnt, 2) if gram_cnt else None,
+                                    "GB_s": round(8 * n * K / (1e-3 * gram_ms / gram_cnt) / 1e9, 1) if gram_cnt else None,
+                                    "TFLOP_s_useful": round(n * K * (K + 1) / (1e-3 * gram_ms / gram_cnt) / 1e12, 3)
+                                    if gram_cnt else None}
+                                   if dev.gram_deferred else
+                                   {"mode": "a Gram row of factor 1's new column in every step (from the register row)"}),
             "basis_mul_mfma": {
                 "avg_us": round(mf_s * 1e6, 2),
                 "GB_s": round(vy_bytes / mf_s / 1e9, 1) if mf_cnt else None,

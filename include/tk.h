@@ -134,6 +134,12 @@ int tk_decomp_exchange_signalled(tk_decomp* dc);
  * ran ahead, like tk_solver_run, may have enqueued more steps than its caller has read). */
 int tk_decomp_next_step(tk_decomp* dc);
 
+/* How many times one step of all local factors reads the bytes of A_s: 1 when the factors
+ * share one gather-format A_s and its entries are read once for all of them (CGS2 with the
+ * interleaved SpMV), else the local factor count (benchmark byte
+ * models, SURVEY.md 8(d): "count the CSR bytes once per batch"). */
+int tk_decomp_matrix_reads(tk_decomp* dc);
+
 /* Element-wise max of vals[0..count) over the ranks sharing dc's records exchange (no-op on
  * one rank; count <= 64).  Collective: every rank calls it at the same point of its call
  * sequence.  tk_solver_run agrees its issue depth and worker count with it, so that every
@@ -204,6 +210,23 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out);
 /* Copy V[:, c0 .. c0+nc-1] of local factor f (0-based within this rank) to host
  * (column-major n x nc).  Flushes a pending column first. */
 tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out);
+
+/* orthogonality_loss's Gram matrix (src/orthogonal_bases.jl:231-257) of local factor f:
+ * G = V[:, 0..k)' V[:, 0..k), k <= min(64, kmax+1), column-major k x k on the host (G NULL:
+ * leave it on the device -- benchmarks), as ONE SYRK of the basis on v_mfma_f64_16x16x4f64
+ * (the sum over the n rows runs in the matrix core; partials summed in a fixed order, so the
+ * result is bitwise reproducible).  A pending column is flushed first when k includes it.
+ * This is how a handle with a deferred Gram (tk_decomp_gram_deferred) provides the driver's
+ * orthogonality_data of factor 1 (src/tensor_krylov_method.jl:103): orthogonality_data[k] =
+ * norm(G[0..k, 0..k] - I) for every k from one G, instead of a Gram row in every step. */
+tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G);
+/* 1 when global factor 0's Gram rows are NOT carried in the step records (its record's
+ * "tracked" field is 0) and orthogonality_data comes from tk_decomp_gram at the end: the
+ * default for TK_LANCZOS with kmax < 64 (the one-sweep Lanczos step reads no basis row; a
+ * per-step Gram row would stream the tracked factor's whole basis every step).
+ * TKHIP_GRAM=rows | deferred at create overrides it for TK_ARNOLDI / TK_LANCZOS;
+ * TK_LANCZOS_REORTH (its loss check drives the redo) and track_all_gram keep rows. */
+int tk_decomp_gram_deferred(tk_decomp* dc);
 
 /* basis_tensor_mul! (src/utils.jl:478-488, called at src/tensor_krylov_method.jl:112):
  * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).

@@ -71,7 +71,7 @@ tk_status tk_fail_internal(int code, const char* msg) { return fail(code, "%s", 
 
 // ------------------------------------------------------------------ context
 enum { TCLS_STEP = 0, TCLS_PASS1 = 1, TCLS_PASS2 = 2, TCLS_FIN = 3, TCLS_RED = 4, TCLS_VY = 5, TCLS_XCH = 6,
-       TCLS_SWEEP = 7, TCLS_N = 8 };
+       TCLS_SWEEP = 7, TCLS_GRAM = 8, TCLS_N = 9 };
 
 struct tk_ctx {
     int device = 0;
@@ -649,6 +649,10 @@ struct tk_decomp {
     int bk_j = -1;
     KArgs bk_args;
     bool mfspmv = false;    // CGS2 factors sharing one A_s: one gather per nonzero for all (k_spmv_mf)
+    // orthogonality_data of global factor 0 (src/tensor_krylov_method.jl:103) from one MFMA SYRK
+    // of its basis when asked (tk_decomp_gram) instead of a Gram row per step (TKHIP_GRAM)
+    bool gram_deferred = false;
+    double* gram_scr = nullptr;
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -718,6 +722,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->scratch) hipFree(dc->scratch);
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
+    if (dc->gram_scr) hipFree(dc->gram_scr);
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
@@ -789,6 +794,18 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         const char* e = getenv("TKHIP_FIN_D");
         dc->fin_d = !(e && e[0] == '0');
     }
+    {
+        // Gram rows per step (the loss check of LanczosReorth needs them; track_all_gram asks
+        // for every factor's) or one SYRK of factor 0's basis at the end (k <= 64 columns on
+        // MFMA): the default for TensorLanczos, whose one-sweep step reads no basis row but the
+        // tracked factor's Gram row would stream all of it (TKHIP_GRAM=rows / deferred
+        // overrides for both methods)
+        const char* e = getenv("TKHIP_GRAM");
+        bool def = method == TK_LANCZOS;
+        if (e && strcmp(e, "rows") == 0) def = false;
+        if (e && strcmp(e, "deferred") == 0) def = true;
+        dc->gram_deferred = def && method != TK_LANCZOS_REORTH && !track_all_gram && kmax + 1 <= 64;
+    }
     dc->mats.assign(mats, mats + nf);
     dc->hf.resize(nf);
     const int KP = kmax + 2, KC = kmax + 1;
@@ -844,7 +861,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.ctr, 16);
         DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
         const int gi = first_factor + f;
-        d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || gi == 0) ? 1 : 0;
+        d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || (gi == 0 && !dc->gram_deferred)) ? 1 : 0;
         d.gidx = gi;
         d.Uint = nullptr;
         d.AU = nullptr;
@@ -993,6 +1010,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
 int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0; }
 
 int tk_decomp_next_step(tk_decomp* dc) { return dc ? dc->jnext : -1; }
+
+int tk_decomp_matrix_reads(tk_decomp* dc) { return !dc ? -1 : (dc->mfspmv ? 1 : dc->nf); }
+
+int tk_decomp_gram_deferred(tk_decomp* dc) { return dc && dc->gram_deferred ? 1 : 0; }
 
 tk_status tk_decomp_set_replica(tk_decomp* dc, int replica) { TK_API_BEGIN
     CHECKARG(dc, "NULL handle");
@@ -1617,6 +1638,53 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
         HIPCHK(hipMemcpy(out + (size_t)cc * dc->n, dc->scratch, (size_t)dc->n * m * sizeof(double),
                          hipMemcpyDeviceToHost));
     }
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
+    CHECKARG(dc, "NULL argument");
+    CHECKARG(f >= 0 && f < dc->nf, "factor out of range");
+    CHECKARG(k >= 1 && k <= 64 && k <= dc->kmax + 1, "k out of range [1, min(64, kmax+1)]");
+    tk_ctx* c = dc->ctx;
+    HIPCHK(hipSetDevice(c->device));
+    if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
+    // every column the product reads must be in V: flush a pending (or column-buffered) one
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+                      dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
+    if (dc->pending && k - 1 >= dc->last_j + (in_e ? 0 : 1)) {
+        tk_status st = tk_decomp_flush(dc, nullptr);
+        if (st) return st;
+    }
+    if (!dc->gram_scr) HIPCHK(hipMalloc((void**)&dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double)));
+    hipStream_t s = c->stream;
+    {
+        Timer tm(c, TCLS_GRAM, 1);
+        KArgs a = base_args(dc, 0, 0);
+        launch_gram(dc->df, f, a, k, dc->gram_scr, s);
+    }
+    LAUNCHCHK("gram");
+    if (!G) return TK_OK;
+    const int nv = gram_values(k);
+    std::vector<double> v(nv);
+    HIPCHK(hipMemcpyAsync(v.data(), dc->gram_scr + gram_result_offset(dc->ntiles, k), nv * sizeof(double),
+                          hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // k_gram's layout: group pair i (ga <= gb), register r, lane l -> G[col(ga, m), col(gb, n)]
+    // with m = (l>>4) + 4r, n = l&15, col(g, x) = 32 (g>>1) + 2x + (g&1)
+    const int ngr = k <= 32 ? 2 : 4;
+    auto col = [](int g, int x) { return 32 * (g >> 1) + 2 * x + (g & 1); };
+    int i = 0;
+    for (int ga = 0; ga < ngr; ++ga)
+        for (int gb = ga; gb < ngr; ++gb, ++i)
+            for (int r = 0; r < 4; ++r)
+                for (int l = 0; l < 64; ++l) {
+                    const int p = col(ga, (l >> 4) + 4 * r), q = col(gb, l & 15);
+                    if (p >= k || q >= k) continue;
+                    const double x = v[(size_t)(i * 4 + r) * 64 + l];
+                    G[(size_t)q * k + p] = x;
+                    G[(size_t)p * k + q] = x;
+                }
     return TK_OK;
     TK_API_END
 }

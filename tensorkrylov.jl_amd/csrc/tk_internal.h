@@ -166,6 +166,15 @@ void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, doubl
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s);
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s);
+// G = V_f[:, 0..k)' V_f[:, 0..k) on MFMA (k <= 64), into scratch (gram_scratch_doubles(ntiles)):
+// gram_values(k) results at scratch + gram_result_offset, layout of k_gram (tk_kernels.hip)
+int gram_values(int k);
+int gram_blocks(int ntiles);
+size_t gram_scratch_doubles(int ntiles);
+inline size_t gram_result_offset(int ntiles, int k) {
+    return (size_t)(gram_blocks(ntiles) + 32) * gram_values(k);
+}
+void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s);
 
 // record field offsets (see include/tk.h)
 __host__ __device__ inline int rec_len(int kmax) { return 2 * kmax + 10; }

@@ -2182,6 +2182,81 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
     fin_d_tile<MAXC, MODE, true>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
 }
 
+// ------------------------------------------------------------------ orthogonality Gram on MFMA
+// G = V_s[:, 0..k)' V_s[:, 0..k) of one factor (orthogonality_loss, src/orthogonal_bases.jl:
+// 231-257; the driver's orthogonality_data of factor 1, src/tensor_krylov_method.jl:103) as a
+// SYRK on v_mfma_f64_16x16x4f64 (k <= 64): the MFMA's k-dimension runs over 4 basis rows, so
+// the sum over n -- what per-step Gram rows spend DPP reduce-scatters on -- happens in the
+// matrix core, and the basis is read once for all k columns instead of once per step.
+// One dwordx4 per lane fetches V[row, 2p .. 2p+1] of the paired-column tile: lane l (row slot
+// l>>4 of a 4-row quad, pair p = 16b + (l&15)) feeds column group 2b (even columns of 32-column
+// block b) and 2b+1 (odd columns).  For group pairs ga <= gb:
+//   A = V[4 rows, group ga]'   lane l: column (l&15) of ga, row slot l>>4
+//   B = V[4 rows, group gb]    lane l: row slot l>>4, column (l&15) of gb
+//   D[m][n] = G[col(ga, m)][col(gb, n)],  lane l, reg i: m = (l>>4) + 4i, n = l&15,
+// col(g, i) = 32 (g>>1) + 2i + (g&1).  Blocks walk tiles (tile += gridDim.x, the grid a
+// function of n only); the 4 waves' accumulators are summed in fixed order through LDS and
+// each block writes its partial Pg[block][value]; k_gram_reduce sums partials in block order.
+template <int NBLK>
+__global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs a, int f, int k,
+                                              double* __restrict__ Pg) {
+    constexpr int NGR = 2 * NBLK;
+    constexpr int NT = NGR * (NGR + 1) / 2;
+    __shared__ double red[NT * 4 * 64];
+    const DFac& d = F[f];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, kr = lane >> 4, ci = lane & 15;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    f64x4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(k));
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            const int row = w * 64 + q * 4 + kr;
+            double v[NGR];
+#pragma unroll
+            for (int b = 0; b < NBLK; ++b) {
+                const int p = 16 * b + ci;
+                const d2_t x = bld2(tv, ((uint32_t)p * TPB + row) * 16u);   // pairs past k read 0
+                v[2 * b] = 2 * p < k ? x.x : 0.0;
+                v[2 * b + 1] = 2 * p + 1 < k ? x.y : 0.0;                   // (odd column k: stale)
+            }
+            int i = 0;
+#pragma unroll
+            for (int ga = 0; ga < NGR; ++ga)
+#pragma unroll
+                for (int gb = ga; gb < NGR; ++gb, ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i], 0, 0, 0);
+        }
+    }
+    // waves 0, 1, 2, 3 summed in this order
+    for (int ww = 0; ww < 4; ++ww) {
+        if (w == ww) {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int e = (i * 4 + r) * 64 + lane;
+                    red[e] = ww == 0 ? acc[i][r] : red[e] + acc[i][r];
+                }
+        }
+        __syncthreads();
+    }
+    for (int e = threadIdx.x; e < NT * 256; e += 256) GP(double, Pg)[(int64_t)blockIdx.x * NT * 256 + e] = red[e];
+}
+
+// out[s][v] = sum over partials b in [s*seg, min(nb, (s+1)*seg)) of P[b][v], in b order
+__global__ __launch_bounds__(256) void k_gram_reduce(const double* __restrict__ P, int nb, int nv, int seg,
+                                                     double* __restrict__ out) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= nv) return;
+    const int b0 = blockIdx.y * seg, b1 = min(nb, b0 + seg);
+    double s = 0.0;
+    for (int b = b0; b < b1; ++b) s += ld(P, (int64_t)b * nv + v);
+    st(out, (int64_t)blockIdx.y * nv + v, s);
+}
+
 // ------------------------------------------------------------------ plain SpMV (test hook)
 template <int FMT>
 __global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ x, double* __restrict__ y) {
@@ -2438,6 +2513,24 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
     else
         hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
 }
+int gram_values(int k) { return k <= 32 ? 3 * 256 : 10 * 256; }
+int gram_blocks(int ntiles) { return ntiles < 512 ? ntiles : 512; }
+size_t gram_scratch_doubles(int ntiles) { return (size_t)(gram_blocks(ntiles) + 32 + 1) * 10 * 256; }
+void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s) {
+    const int nb = gram_blocks(a.ntiles), nv = gram_values(k);
+    double* P = scratch;
+    double* Q = P + (size_t)nb * nv;
+    double* out = Q + (size_t)32 * nv;
+    if (k <= 32)
+        hipLaunchKernelGGL(k_gram<1>, dim3(nb), dim3(256), 0, s, F, a, f, k, P);
+    else
+        hipLaunchKernelGGL(k_gram<2>, dim3(nb), dim3(256), 0, s, F, a, f, k, P);
+    // two fixed-order levels: segments of 16 partials, then the segment sums
+    const int seg = 16, nseg = (nb + seg - 1) / seg;
+    hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 255) / 256, nseg), dim3(256), 0, s, P, nb, nv, seg, Q);
+    hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 255) / 256, 1), dim3(256), 0, s, Q, nseg, nv, nseg, out);
+}
+
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
     const int nb = (int)((A.n + TPB - 1) / TPB);
     const int fmt = A.ndiag > 0 ? (A.ndiag <= 4 ? (A.toep ? SPM_DIAT : SPM_DIA) : SPM_DIAN) : (A.sell ? SPM_SELL : SPM_CSR);

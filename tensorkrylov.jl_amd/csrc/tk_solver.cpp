@@ -59,6 +59,8 @@ struct tk_solver {
     std::vector<double> H;        // [s][c * KP + r]  (H_s, (kmax+2) x (kmax+1), column-major)
     std::vector<double> bt;       // [s][c]
     std::vector<double> gram0;    // factor 0's Gram rows: [c * KC + i], i <= c
+    bool gram_tracked = false;    // factor 0's records carry Gram rows (else: a deferred Gram,
+                                  // tk_decomp_gram; orthogonality_data is filled by the caller)
     std::vector<double> loss;     // [s][j] LanczosReorth loss of step j
     std::vector<unsigned char> reorth;
     IterResult last;
@@ -108,8 +110,10 @@ static void apply_record(tk_solver* sv, int j, const double* rec) {
         const int c = (int)lround(r[o_col]);
         if (c >= 0 && c < KC) {
             sv->bt[(size_t)s * KC + c] = r[o_bt];                 // update_rhs! (src/utils.jl:466-476)
-            if (s == 0 && r[o_tracked] > 0)
+            if (s == 0 && r[o_tracked] > 0) {
+                sv->gram_tracked = true;
                 for (int i = 0; i <= c; ++i) sv->gram0[(size_t)c * KC + i] = r[o_gram + i];
+            }
         }
     }
 }
@@ -143,7 +147,12 @@ static void evaluate(const tk_solver* sv, int k, IterResult& out, Work& ws) {
         return;
     }
     out.rel = out.r_norm / sv->bnorm;                              // :99
-    // orthogonality_loss(V_1, k) = norm(V'V - I) from the lower Gram rows (:103)
+    // orthogonality_loss(V_1, k) = norm(V'V - I) from the lower Gram rows (:103); NaN when
+    // factor 0's Gram is deferred (the caller fills orthogonality_data from tk_decomp_gram)
+    if (!sv->gram_tracked) {
+        out.orth = NAN;
+        return;
+    }
     double acc = 0.0;
     for (int c = 0; c < k; ++c) {
         const double* g = &sv->gram0[(size_t)c * KC];

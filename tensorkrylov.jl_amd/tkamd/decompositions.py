@@ -181,6 +181,9 @@ class TensorDecomposition:
 
     def orthogonality_loss(self, s, k):
         from .compressed import orthogonality_loss_from_gram
+        if s not in self.gram and s == 0 and getattr(self.dev, "gram_deferred", False):
+            # no Gram rows in the records: one SYRK of the basis (tk_decomp_gram)
+            return orthogonality_loss_from_gram(self.dev.gram(0, k), k)
         return orthogonality_loss_from_gram(self.gram[s], k)
 
     def basis(self, s, k):

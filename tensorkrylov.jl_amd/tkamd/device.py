@@ -145,6 +145,25 @@ class DeviceDecomposition:
         enqueued, possibly by a driver that ran ahead of the records read so far."""
         return int(self.ctx._lib.tk_decomp_next_step(self.h))
 
+    @property
+    def matrix_reads(self):
+        """Reads of A_s's bytes per step of all local factors (tk_decomp_matrix_reads): 1 when
+        factors sharing one A_s read it once for all, else the local factor count."""
+        return int(self.ctx._lib.tk_decomp_matrix_reads(self.h))
+
+    @property
+    def gram_deferred(self):
+        """Factor 0's Gram comes from one SYRK (gram()) rather than per-step record rows
+        (tk_decomp_gram_deferred)."""
+        return bool(self.ctx._lib.tk_decomp_gram_deferred(self.h))
+
+    def gram(self, f, k, want=True):
+        """G = V_f[:, :k]' V_f[:, :k] of local factor f on MFMA (tk_decomp_gram); want=False
+        leaves it on the device."""
+        G = np.zeros((k, k)) if want else None
+        L.check(self.ctx._lib.tk_decomp_gram(self.h, int(f), int(k), L.dptr(G)))
+        return G.T.copy() if want else None
+
     def set_replica(self, on=True):
         """This rank's factors are replicas of another rank's (tk_decomp_set_replica): same
         steps, zero rows sent into the records all-reduce."""

@@ -113,15 +113,18 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             rel = r_norm / b_norm                                   # :99
             conv.relative_residual_norm[k - 1] = rel
             conv.projected_residual_norm[k - 1] = r_comp
-            conv.orthogonality_data[k - 1] = td.orthogonality_loss(0, k)          # :103
+            if not _gram_deferred(td):
+                conv.orthogonality_data[k - 1] = td.orthogonality_loss(0, k)      # :103
             if rel < tol:                                           # :108-118
                 # basis_tensor_mul! on the device; X sized by ncomponents(y)
                 # (the reference sizes it by approxdata.rank, SURVEY.md 3.2 deviation)
                 x = _solution(td, k, lam, Ys)
+                _fill_deferred_orthogonality(conv, td, k)
                 conv.timing["loop_s"] = time.perf_counter() - t_loop
                 if verbose:
                     print("Convergence")
                 return x
+        _fill_deferred_orthogonality(conv, td, nmax)
         conv.timing["loop_s"] = time.perf_counter() - t_loop
         if verbose:
             print("No convergence")
@@ -131,6 +134,31 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             conv.decomposition = td
         else:
             td.close()
+
+
+def _gram_deferred(td):
+    return bool(getattr(td.dev, "gram_deferred", False))
+
+
+def _fill_deferred_orthogonality(conv, td, k_last):
+    """orthogonality_data[k] = orthogonality_loss(V_1, k) (src/tensor_krylov_method.jl:103,
+    src/orthogonal_bases.jl:250-257) for k = 2..k_last, from ONE Gram matrix of factor 1's
+    basis (tk_decomp_gram: a SYRK on the matrix cores) when the handle does not carry a Gram
+    row per step (tk_decomp_gram_deferred).  The values are those the reference computes at
+    iteration k: columns 1..k are final once step k is done.  With several ranks the rank
+    owning factor 1 computes them and one all-reduce (every rank calls it here) shares them."""
+    if not _gram_deferred(td) or k_last < 2:
+        return
+    from .compressed import orthogonality_loss_from_gram
+    part = td.part
+    orth = np.zeros(k_last)
+    if part.first == 0 and part.nf > 0 and not part.replica:
+        G = td.dev.gram(0, k_last)
+        for k in range(2, k_last + 1):
+            orth[k - 1] = orthogonality_loss_from_gram(G, k)
+    if part.nranks > 1:
+        orth = td.ctx.allreduce_host(orth)
+    conv.orthogonality_data[1:k_last] = orth[1:k_last]
 
 
 def _solution(td, k, lam, Ys):
@@ -179,6 +207,7 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
     if outcome == 1:                                                # :108-118
         lam, Ys = sv.solution(k_end)
         x = _solution(td, k_end, lam, Ys)
+    _fill_deferred_orthogonality(conv, td, k_end)
     conv.timing["loop_s"] = time.perf_counter() - t_loop
     # the host mirror of H, b~ and factor 1's Gram rows (principal_minors readers)
     H, bt, G = sv.state()

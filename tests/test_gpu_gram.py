@@ -1,0 +1,89 @@
+"""orthogonality_loss's Gram matrix as one MFMA SYRK (tk_decomp_gram, k_gram) and the deferred
+orthogonality_data of factor 1 built from it (src/orthogonal_bases.jl:231-257,
+src/tensor_krylov_method.jl:103).
+
+G = V[:, :k]' V[:, :k] on v_mfma_f64_16x16x4f64 must equal the host product of the basis the
+device holds (entries are O(1) on the diagonal and O(eps) off it: absolute 1e-14 at n = 5000,
+1e-13 at n = 2^20, where each entry sums 2^20 products); k crosses the 32-column block edge
+and odd k exercises the masked last column of a pair.  The driver's orthogonality_data with
+a deferred Gram (TensorLanczos' default) must be rounding noise of the same size as with a
+Gram row per step, and the rest of the trajectory bitwise the same.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _tk():
+    import tkamd
+    return tkamd
+
+
+@pytest.mark.parametrize("method", [0, 1])
+def test_gram_matches_host_product(ctx, method):
+    tk = _tk()
+    n, K, d = 5000, 50, 2
+    csc = tk.assemble_matrix(n, "Laplace")
+    rng = np.random.default_rng(21)
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    A = tk.DeviceMatrix(ctx, csc)
+    dev = tk.DeviceDecomposition(ctx, method, d, 0, [A] * d, bs, K)
+    dev.init(False)
+    dev.sweep(0, K)
+    for k in (1, 2, 7, 31, 32, 33, 50, 51):
+        G = dev.gram(1, k)
+        V = dev.basis(1, 0, k)
+        ref = V.T @ V
+        assert G.shape == (k, k)
+        assert np.array_equal(G, G.T)
+        assert np.abs(G - ref).max() <= 1e-14, (k, np.abs(G - ref).max())
+    # bitwise reproducible
+    assert np.array_equal(dev.gram(0, 50), dev.gram(0, 50))
+    dev.close()
+    A.close()
+
+
+def test_gram_full_size(ctx):
+    """n = 2^20 (the C2 factor size), k = 51."""
+    tk = _tk()
+    n, K = 1 << 20, 50
+    csc = tk.assemble_matrix(n, "Laplace")
+    b = np.random.default_rng(1000).random(n)
+    A = tk.DeviceMatrix(ctx, csc)
+    dev = tk.DeviceDecomposition(ctx, 0, 1, 0, [A], [b / np.linalg.norm(b)], K)
+    dev.init(False)
+    dev.sweep(0, K)
+    G = dev.gram(0, K + 1)
+    V = dev.basis(0, 0, K + 1)
+    ref = V.T @ V
+    assert np.abs(G - ref).max() <= 1e-13, np.abs(G - ref).max()
+    assert np.abs(G - np.eye(K + 1)).max() <= 1e-12          # the basis is orthonormal
+    dev.close()
+    A.close()
+
+
+@pytest.mark.parametrize("method", ["TensorArnoldi", "TensorLanczos"])
+def test_deferred_orthogonality_data(ctx, method, monkeypatch):
+    tk = _tk()
+    d, n, K = 3, 4000, 40
+    A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
+    b = tk.normalize_rhs(tk.random_rhs(d, n, np.random.default_rng(12345)))
+    out = {}
+    for mode in ("rows", "deferred"):
+        monkeypatch.setenv("TKHIP_GRAM", mode)
+        conv = tk.ConvergenceData(K)
+        tk.tensorkrylov(conv, A, [x.copy() for x in b], 1e-9, K, method, ctx=ctx, keep_decomposition=True)
+        assert conv.decomposition.dev.gram_deferred == (mode == "deferred")
+        conv.decomposition.close()
+        out[mode] = conv
+    r, q = out["rows"], out["deferred"]
+    assert np.array_equal(r.relative_residual_norm, q.relative_residual_norm)
+    assert np.array_equal(r.projected_residual_norm, q.projected_residual_norm)
+    o1, o2 = np.asarray(r.orthogonality_data[1:]), np.asarray(q.orthogonality_data[1:])
+    assert np.all(np.isfinite(o2))
+    if method == "TensorArnoldi":
+        assert np.all(o1 < 1e-12) and np.all(o2 < 1e-12)
+    # the same Gram entries summed in another order: each differs by ~1e-15, the norm over
+    # k^2 entries by at most ~k 1e-14
+    assert np.abs(o1 - o2).max() <= 1e-12, np.abs(o1 - o2).max()
