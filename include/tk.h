@@ -110,9 +110,11 @@ tk_status tk_matvec(tk_mat* A, const double* x, double* y);
  * basis columns instead of n+1).  mats[i], b[i] (length n, host) are factor
  * first_factor+i's A_s and b_s.  All factors share n (src/tensor_krylov_method.jl:46).
  * kmax = nmax; steps j = 0 .. kmax-1 are allowed.
- * track_all_gram != 0 keeps the Gram row of every factor (always on for
- * TK_LANCZOS_REORTH); otherwise only global factor 0's (for the driver's
- * orthogonality_data, src/tensor_krylov_method.jl:103). */
+ * track_all_gram: 1 keeps the Gram row of every factor in the step records (always on for
+ * TK_LANCZOS_REORTH); 2 keeps global factor 0's (the driver's orthogonality_data,
+ * src/tensor_krylov_method.jl:103) for a caller that reads it after every step, like the
+ * reference's loop; 0 lets the library choose between factor 0's rows and a deferred Gram
+ * (tk_decomp_gram_deferred). */
 tk_status tk_decomp_create(tk_ctx* ctx, int method, int d_total, int first_factor, int nf,
                            tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
                            int track_all_gram, tk_decomp** out);

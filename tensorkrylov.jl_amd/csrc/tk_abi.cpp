@@ -804,6 +804,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         bool def = method == TK_LANCZOS;
         if (e && strcmp(e, "rows") == 0) def = false;
         if (e && strcmp(e, "deferred") == 0) def = true;
+        if (track_all_gram == 2) def = false;   // the caller reads factor 1's loss every step
         dc->gram_deferred = def && method != TK_LANCZOS_REORTH && !track_all_gram && kmax + 1 <= 64;
     }
     dc->mats.assign(mats, mats + nf);
@@ -861,7 +862,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.ctr, 16);
         DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
         const int gi = first_factor + f;
-        d.track_gram = (track_all_gram || method == TK_LANCZOS_REORTH || (gi == 0 && !dc->gram_deferred)) ? 1 : 0;
+        d.track_gram = (track_all_gram == 1 || method == TK_LANCZOS_REORTH || (gi == 0 && !dc->gram_deferred)) ? 1 : 0;
         d.gidx = gi;
         d.Uint = nullptr;
         d.AU = nullptr;

@@ -88,7 +88,8 @@ function HIPDecomp(ctx::HIPContext, method::Cint, mats::Vector{HIPMatrix}, b, km
     check(ccall((:tk_decomp_create, libtkhip), Cint,
                 (Ptr{Cvoid}, Cint, Cint, Cint, Cint, Ptr{Ptr{Cvoid}}, Ptr{Ptr{Float64}}, Int64, Cint, Cint,
                  Ref{Ptr{Cvoid}}),
-                ctx.h, method, d, 0, d, [m.h for m in mats], [pointer(x) for x in bs], mats[1].n, kmax, 0, r))
+                ctx.h, method, d, 0, d, [m.h for m in mats], [pointer(x) for x in bs], mats[1].n, kmax,
+                2 #= factor 1's Gram rows per step: orthogonality_loss is read every iteration =#, r))
     dc = HIPDecomp(r[], d, mats[1].n, kmax, reclen(kmax), mats, bs)
     finalizer(x -> ccall((:tk_decomp_destroy, libtkhip), Cint, (Ptr{Cvoid},), x.h), dc)
 end

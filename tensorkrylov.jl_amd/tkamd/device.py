@@ -105,7 +105,9 @@ class DeviceDecomposition:
 
     def __init__(self, ctx, method, d_total, first, mats, bs, kmax, track_all_gram=False, n=None):
         """mats may be empty (a rank of a job with more ranks than factors: it only takes part
-        in the records exchange); n is then required."""
+        in the records exchange); n is then required.  track_all_gram: True/1 = Gram rows of
+        every factor in the records, 2 = factor 0's rows per step, False/0 = the library's
+        choice (tk_decomp_create)."""
         self.ctx = ctx
         self.method = method
         self.d_total = d_total
@@ -122,7 +124,7 @@ class DeviceDecomposition:
         barr = BArr(*[L.dptr(b) for b in self._bs])
         h = ctypes.c_void_p()
         L.check(ctx._lib.tk_decomp_create(ctx.h, int(method), int(d_total), int(first), self.nf, marr,
-                                          barr, int(self.n), int(kmax), 1 if track_all_gram else 0,
+                                          barr, int(self.n), int(kmax), int(track_all_gram),
                                           ctypes.byref(h)))
         self.h = h
         self._mats = mats

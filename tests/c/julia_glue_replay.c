@@ -5,7 +5,7 @@
  * offsets, so the glue's ccall sequence is exercised without a Julia toolchain:
  *
  *   HIPMatrix(ctx, A)       tk_matrix_from_csc(..., one_based = 1)   (Julia's colptr/rowval as-is)
- *   HIPDecomp(...)          tk_decomp_create(ctx, method, d, 0, d, mats, b, n, kmax, 0)
+ *   HIPDecomp(...)          tk_decomp_create(ctx, method, d, 0, d, mats, b, n, kmax, 2)
  *   records(dc, :init)      tk_decomp_init      -> apply_records!(td, rec, -1)
  *   orthonormalize!(td, k)  tk_decomp_step(k-1) -> apply_records!(td, rec, k-1),  k = 1..nmax
  *
@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
         mats[s] = A;                    /* the glue's IdDict cache: one device matrix per A_s object */
         bp[s] = b + (size_t)s * n;
     }
-    CHECK(tk_decomp_create(ctx, method_, d, 0, d, mats, bp, n, kmax, 0, &dc));
+    CHECK(tk_decomp_create(ctx, method_, d, 0, d, mats, bp, n, kmax, 2, &dc));
     const int m = tk_record_len(kmax);
     if (m != 2 * kmax + 10) {           /* reclen(kmax) = 2kmax + 10 in the glue */
         fprintf(stderr, "record length %d != 2kmax+10\n", m);

@@ -50,7 +50,7 @@ def test_c_caller_replays_julia_glue(ctx, method, tmp_path):
     csc = tk.assemble_matrix(n, "Laplace")
     A = tk.KroneckerMatrix(tk.SymInstance, [csc] * d, tk.Laplace)
     td = {"TensorArnoldi": tk.TensorArnoldi, "TensorLanczos": tk.TensorLanczos,
-          "TensorLanczosReorth": tk.TensorLanczosReorth}[method](A, K, ctx=ctx)
+          "TensorLanczosReorth": tk.TensorLanczosReorth}[method](A, K, ctx=ctx, track_all_gram=2)
     td.orthonormalize_first([b.copy() for b in bs])
     for k in range(2, K + 1):
         td.orthonormalize(k)
