@@ -224,8 +224,9 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
 tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G);
 /* 1 when global factor 0's Gram rows are NOT carried in the step records (its record's
  * "tracked" field is 0) and orthogonality_data comes from tk_decomp_gram at the end: the
- * default for TK_LANCZOS with kmax < 64 (the one-sweep Lanczos step reads no basis row; a
- * per-step Gram row would stream the tracked factor's whole basis every step).
+ * default for TK_ARNOLDI / TK_LANCZOS with kmax < 64 (the one-sweep Lanczos step reads no
+ * basis row, so a per-step Gram row would stream the tracked factor's whole basis every step;
+ * for Arnoldi the row's dots make the tracked factor the slowest rank at one factor per GPU).
  * TKHIP_GRAM=rows | deferred at create overrides it for TK_ARNOLDI / TK_LANCZOS;
  * TK_LANCZOS_REORTH (its loss check drives the redo) and track_all_gram keep rows. */
 int tk_decomp_gram_deferred(tk_decomp* dc);

@@ -797,11 +797,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     {
         // Gram rows per step (the loss check of LanczosReorth needs them; track_all_gram asks
         // for every factor's) or one SYRK of factor 0's basis at the end (k <= 64 columns on
-        // MFMA): the default for TensorLanczos, whose one-sweep step reads no basis row but the
-        // tracked factor's Gram row would stream all of it (TKHIP_GRAM=rows / deferred
-        // overrides for both methods)
+        // MFMA), the default: the one-sweep Lanczos step reads no basis row, so a per-step Gram
+        // row streams the tracked factor's whole basis every step; for Arnoldi the row's dots
+        // make the tracked factor's launch the long pole at one factor per GPU (TKHIP_GRAM=rows
+        // restores the rows)
         const char* e = getenv("TKHIP_GRAM");
-        bool def = method == TK_LANCZOS;
+        bool def = true;
         if (e && strcmp(e, "rows") == 0) def = false;
         if (e && strcmp(e, "deferred") == 0) def = true;
         if (track_all_gram == 2) def = false;   // the caller reads factor 1's loss every step

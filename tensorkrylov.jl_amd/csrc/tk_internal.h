@@ -172,7 +172,7 @@ int gram_values(int k);
 int gram_blocks(int ntiles);
 size_t gram_scratch_doubles(int ntiles);
 inline size_t gram_result_offset(int ntiles, int k) {
-    return (size_t)(gram_blocks(ntiles) + 32) * gram_values(k);
+    return (size_t)(gram_blocks(ntiles) + 64) * gram_values(k);
 }
 void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s);
 

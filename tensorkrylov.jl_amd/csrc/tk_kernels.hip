@@ -2209,25 +2209,36 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
     f64x4 acc[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) acc[i] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    const bool ev0 = 2 * ci < k, od0 = 2 * ci + 1 < k, ev1 = 2 * (16 + ci) < k, od1 = 2 * (16 + ci) + 1 < k;
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(k));
-#pragma unroll 4
-        for (int q = 0; q < 16; ++q) {
-            const int row = w * 64 + q * 4 + kr;
-            double v[NGR];
+        // GQ row quads' loads in flight before their MFMAs (pairs past k read 0; the odd
+        // column k of the last pair is stale and masked)
+        constexpr int GQ = 8;
+#pragma unroll 1
+        for (int q0 = 0; q0 < 16; q0 += GQ) {
+            d2_t x[GQ][NBLK];
 #pragma unroll
-            for (int b = 0; b < NBLK; ++b) {
-                const int p = 16 * b + ci;
-                const d2_t x = bld2(tv, ((uint32_t)p * TPB + row) * 16u);   // pairs past k read 0
-                v[2 * b] = 2 * p < k ? x.x : 0.0;
-                v[2 * b + 1] = 2 * p + 1 < k ? x.y : 0.0;                   // (odd column k: stale)
+            for (int q = 0; q < GQ; ++q)
+#pragma unroll
+                for (int b = 0; b < NBLK; ++b)
+                    x[q][b] = bld2(tv, ((uint32_t)(16 * b + ci) * TPB + w * 64 + (q0 + q) * 4 + kr) * 16u);
+#pragma unroll
+            for (int q = 0; q < GQ; ++q) {
+                double v[NGR];
+                v[0] = ev0 ? x[q][0].x : 0.0;
+                v[1] = od0 ? x[q][0].y : 0.0;
+                if (NBLK > 1) {
+                    v[NBLK > 1 ? 2 : 0] = ev1 ? x[q][NBLK - 1].x : 0.0;
+                    v[NBLK > 1 ? 3 : 1] = od1 ? x[q][NBLK - 1].y : 0.0;
+                }
+                int i = 0;
+#pragma unroll
+                for (int ga = 0; ga < NGR; ++ga)
+#pragma unroll
+                    for (int gb = ga; gb < NGR; ++gb, ++i)
+                        acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i], 0, 0, 0);
             }
-            int i = 0;
-#pragma unroll
-            for (int ga = 0; ga < NGR; ++ga)
-#pragma unroll
-                for (int gb = ga; gb < NGR; ++gb, ++i)
-                    acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i], 0, 0, 0);
         }
     }
     // waves 0, 1, 2, 3 summed in this order
@@ -2513,14 +2524,17 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
     else
         hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
 }
+#ifndef TK_GRAM_BLOCKS
+#define TK_GRAM_BLOCKS 1024   // k_gram blocks (4 per CU): a function of n only
+#endif
 int gram_values(int k) { return k <= 32 ? 3 * 256 : 10 * 256; }
-int gram_blocks(int ntiles) { return ntiles < 512 ? ntiles : 512; }
-size_t gram_scratch_doubles(int ntiles) { return (size_t)(gram_blocks(ntiles) + 32 + 1) * 10 * 256; }
+int gram_blocks(int ntiles) { return ntiles < TK_GRAM_BLOCKS ? ntiles : TK_GRAM_BLOCKS; }
+size_t gram_scratch_doubles(int ntiles) { return (size_t)(gram_blocks(ntiles) + 64 + 1) * 10 * 256; }
 void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s) {
     const int nb = gram_blocks(a.ntiles), nv = gram_values(k);
     double* P = scratch;
     double* Q = P + (size_t)nb * nv;
-    double* out = Q + (size_t)32 * nv;
+    double* out = Q + (size_t)64 * nv;
     if (k <= 32)
         hipLaunchKernelGGL(k_gram<1>, dim3(nb), dim3(256), 0, s, F, a, f, k, P);
     else
