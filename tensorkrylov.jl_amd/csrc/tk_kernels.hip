@@ -560,60 +560,36 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 // ------------------------------------------------------------------ one A_s, many factors
 // The CGS2 first pass of factors sharing one A_s (the C3 gallery: five factors, one random
 // sparse matrix) is bound by its random gathers of U: ~15 distinct cache lines per row per
-// factor move from L2 to L1 for 8 useful bytes each.  Interleaving the factors' U rows
-// (Uint[r][f], k_ilv) lets one gather per nonzero fetch the entries of every factor, and
-// k_spmv_mf writes each factor's A U with the same products and sums in the same order as its
-// own SpMV would (bitwise the same), which pass 1 then reads as one more streamed vector.
-// F[0] carries the group's Uint (all factors' descriptors point to it).
+// factor move from L2 to L1 for 8 useful bytes each.  With the factors' U rows interleaved
+// (Uint[r][f], written by k_arn_a2 beside U) one gather per nonzero fetches the entries of
+// every factor, and k_spmv_mf writes each factor's A U with the same products and sums in the
+// same order as its own SpMV would (bitwise the same), which pass 1 then reads as one more
+// streamed vector.  F[0] carries the group's Uint (all factors' descriptors point to it).
 // Uint rows are padded to ilv_pitch(nf) doubles (a power of two: one aligned 16..64-byte
-// piece per gather, read as 16-byte loads)
+// piece per row, read as 16-byte loads; the padding stays zero from the allocation).
 __host__ __device__ inline int ilv_pitch(int nf) { return nf <= 2 ? 2 : (nf <= 4 ? 4 : 8); }
-// One 256-row tile per block (ld_ is a multiple of 256): the factors' entries are transposed
-// through LDS so every wave store writes 1 KiB of contiguous Uint (row-strided 16-byte
-// stores left each line to be completed by four separate instructions)
-__global__ __launch_bounds__(TPB) void k_ilv(const DFac* __restrict__ F, int nf, int64_t ld_) {
-    __shared__ double tl[TPB * 9];   // row pitch 9: the transposing writes are conflict-free
-    const int64_t r0 = (int64_t)blockIdx.x * TPB;
-    const int t = threadIdx.x;
-    double* Ui = F[0].Uint;
-    const int p = ilv_pitch(nf);
-    double u[8];
-#pragma unroll
-    for (int f = 0; f < 8; ++f) u[f] = f < nf ? ld(F[f < nf ? f : 0].U, r0 + t) : 0.0;
-#pragma unroll
-    for (int f = 0; f < 8; ++f)
-        if (f < p) tl[t * 9 + f] = u[f];
-    __syncthreads();
-    const int nch = TPB * p / 2;   // 16-byte pieces of the tile's Uint rows
-    auto* out = GP(d2_t, Ui + r0 * p);
-    for (int c = t; c < nch; c += TPB) {
-        const int e = 2 * c, row = e / p, col = e - row * p;
-        out[c] = (d2_t){tl[row * 9 + col], tl[row * 9 + col + 1]};
-    }
-}
+// Four lanes per row (tools/gatherprobe.hip: one thread per row with three 16-byte gathers
+// per nonzero ran at 0.88 of the pattern's random-gather ceiling, four lanes at 0.98): lane p
+// of a row's quad gathers piece p (16 bytes, factors 2p and 2p+1) of the row's Uint entry, so a
+// wave instruction touches 16 rows' 64-byte pieces instead of 64 rows' -- and sums its two
+// factors in the row's order (ascending column, products and sums rounded apart: bitwise the
+// per-factor SpMV).  64 rows per 256-thread block.
 template <int FMT, int NFM>
 __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int nf, KArgs a) {
 #pragma clang fp contract(off)
-    const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+    constexpr int NP = NFM <= 2 ? 2 : (NFM <= 4 ? 4 : 8);   // = ilv_pitch(NFM)
+    constexpr int NQ = (NFM + 1) / 2;                        // lanes of a quad with factors
+    const int p = threadIdx.x & 3;
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 4) + (threadIdx.x >> 2);
     if (r >= a.ld) return;
     const DFac& d0 = F[0];
     const double* Ui = d0.Uint;
-    constexpr int NP = NFM <= 2 ? 2 : (NFM <= 4 ? 4 : 8);   // = ilv_pitch(NFM)
-    double s[NFM];
-#pragma unroll
-    for (int f = 0; f < NFM; ++f) s[f] = 0.0;
-    if (r < a.n) {
-        // the per-row order of spmv<FMT> (ascending column, products and sums rounded apart)
-        auto acc1 = [&](double v, int64_t c) {
-            double u[NFM];
-#pragma unroll
-            for (int f = 0; f < NFM; f += 2) {
-                const d2_t x = GP(const d2_t, Ui + c * NP)[f >> 1];
-                u[f] = x.x;
-                if (f + 1 < NFM) u[f + 1] = x.y;
-            }
-#pragma unroll
-            for (int f = 0; f < NFM; ++f) s[f] = add_rn(s[f], mul_rn(v, u[f]));
+    double s0 = 0.0, s1 = 0.0;
+    if (r < a.n && p < NQ) {
+        auto acc = [&](double v, int64_t c) {
+            const d2_t x = GP(const d2_t, Ui + c * NP)[p];
+            s0 = add_rn(s0, mul_rn(v, x.x));
+            s1 = add_rn(s1, mul_rn(v, x.y));
         };
         const SpM& A = d0.A;
         if (FMT == SPM_SELL) {
@@ -622,8 +598,8 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
             const int64_t base = GP(const long long, A.sptr)[t];
             const int w = GP(const int, A.swidth)[t];
             const int len = GP(const int, A.rowlen)[r];
-            // slots in groups of SG: their indices and values, then all their gathers, are in
-            // flight together before the products are summed in order
+            // slots in groups of SG: their indices and values, then their gathers, in flight
+            // together before the products are summed in order
             constexpr int SG = 4;
             for (int q0 = 0; q0 < w; q0 += SG) {
                 int64_t cc[SG];
@@ -635,28 +611,26 @@ __global__ __launch_bounds__(TPB) void k_spmv_mf(const DFac* __restrict__ F, int
                     cc[g] = in ? (int64_t)GP(const int, A.scol)[e] : -1;
                     vv[g] = in ? ld(A.sval, e) : 0.0;
                 }
-                double u[SG][NFM];
+                d2_t x[SG];
 #pragma unroll
                 for (int g = 0; g < SG; ++g)
+                    x[g] = cc[g] >= 0 ? GP(const d2_t, Ui + cc[g] * NP)[p] : (d2_t){0.0, 0.0};
 #pragma unroll
-                    for (int f = 0; f < NFM; f += 2) {
-                        const d2_t x = cc[g] >= 0 ? GP(const d2_t, Ui + cc[g] * NP)[f >> 1] : (d2_t){0.0, 0.0};
-                        u[g][f] = x.x;
-                        if (f + 1 < NFM) u[g][f + 1] = x.y;
+                for (int g = 0; g < SG; ++g)
+                    if (cc[g] >= 0) {
+                        s0 = add_rn(s0, mul_rn(vv[g], x[g].x));
+                        s1 = add_rn(s1, mul_rn(vv[g], x[g].y));
                     }
-#pragma unroll
-                for (int g = 0; g < SG; ++g)
-                    if (cc[g] >= 0)
-#pragma unroll
-                        for (int f = 0; f < NFM; ++f) s[f] = add_rn(s[f], mul_rn(vv[g], u[g][f]));
             }
         } else {
             const int p0 = GP(const int, A.rowptr)[r], p1 = GP(const int, A.rowptr)[r + 1];
-            for (int p = p0; p < p1; ++p) acc1(ld(A.val, p), (int64_t)GP(const int, A.col)[p]);
+            for (int q = p0; q < p1; ++q) acc(ld(A.val, q), (int64_t)GP(const int, A.col)[q]);
         }
     }
-#pragma unroll
-    for (int f = 0; f < NFM; ++f) st(F[f].AU, r, s[f]);
+    if (p < NQ) {
+        st(F[2 * p].AU, r, s0);
+        if (2 * p + 1 < NFM) st(F[2 * p + 1 < NFM ? 2 * p + 1 : 0].AU, r, s1);
+    }
 }
 
 // ------------------------------------------------------------------ Arnoldi (CGS2)
@@ -744,6 +718,10 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2(const DFac* __r
         const double w = ld(d.W, r);
         const double u = ok ? (w - row_dot<MAXC, SC>(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
+        // factors sharing A_s: also the interleaved row the next step's k_spmv_mf gathers
+        // (the group's blocks of one tile range run on one XCD -- npart is a multiple of 8 --
+        // so its L2 merges their 8-byte pieces of each row)
+        if (d.Uint) st(d.Uint, r * ilv_pitch(d.inf) + d.ifs, u);
         reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
         const double e[2] = {u * u, vj * ld(d.b, r)};
         reduce_scalars<2>(e, tr, acc, nc, first);
@@ -2340,8 +2318,8 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 }
 void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
-    const int nb = (int)((a.ld + TPB - 1) / TPB);
-    hipLaunchKernelGGL(k_ilv, dim3(nb), dim3(TPB), 0, s, F, nf, a.ld);
+    // (Uint is written by the previous step's k_arn_a2: no interleaving pass)
+    const int nb = (int)((a.ld + TPB / 4 - 1) / (TPB / 4));
     auto go = [&](auto FM) {
         constexpr int FMv = decltype(FM)::value;
         switch (nf) {   // the group size is a template parameter (2..8 factors)

@@ -1,0 +1,14 @@
+# C3 changes: the shared-matrix tests, the C3 config parity, then the C3 bench and kernel stats
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -x -v -k "shared_matrix or C3 or RandSparse" --timeout 300 --timeout-method thread > gpurun_out/t_c3.log 2>&1
+rc=$?; echo "pytest EXIT $rc" >> gpurun_out/t_c3.log
+grep -E "PASSED|FAILED|ERROR" gpurun_out/t_c3.log | tail -20; tail -2 gpurun_out/t_c3.log
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 300 python bench.py --config C3 --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/bench_C3.log 2>&1 || { echo "bench C3 failed"; tail -5 gpurun_out/bench_C3.log; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/bench_C3.log').read().strip().split('\n')[-1]); print('C3', d['value'], d['roofline']['frac'], d['roofline']['avg_launch_us'], {k:v['avg_us'] for k,v in d['kernels'].items()})"
+cd /tmp && export TMPDIR=/tmp
+rm -rf $R/gpurun_out/prof_c3
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c3 -o run -- python3 $R/bench.py --config C3 --steps 2 --warmup 1 --no-cpu-baseline --no-end-to-end > $R/gpurun_out/prof_c3.log 2>&1 || { echo "rocprof failed"; exit 1; }
+find $R/gpurun_out/prof_c3 -name "*kernel_stats.csv" | head -1 | xargs head -14
