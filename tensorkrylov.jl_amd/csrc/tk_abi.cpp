@@ -1360,7 +1360,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // alpha_j, beta_j and writes the step's record (no post launch)
         a.ubuf = j & 1;
         RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->npd, s), "lan_1s");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 4 + j, 0, s, 0, RED_LAN, &ax), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, 0, s, 0, RED_LAN, &ax), "reduce");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;

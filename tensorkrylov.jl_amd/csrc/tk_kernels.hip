@@ -1177,7 +1177,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     }
     const double uo = own ? u : 0.0, vo = own ? vj : 0.0;
     {
-        double x[16] = {uo * vj, uo * u, vo * vj, vo * bv};
+        // beta_j = ||u - alpha_j v_j|| is taken from dots of wt = u - alpha_{j-1} v_j (alpha_{j-1}
+        // estimates alpha_j): ||wt + (alpha_{j-1} - alpha_j) v_j||^2 expands without the
+        // |u|^2 - alpha^2 cancellation that loses eps (alpha/beta)^2 relative when |alpha| >> beta
+        const double wt = own ? u - alpha * vj : 0.0;
+        double x[16] = {uo * vj, uo * u, vo * vj, vo * bv, wt * wt, wt * vj};
         D1_ACC(0, x);
     }
     if (gram) {
@@ -1200,10 +1204,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         for (int p = 0; p < D1_NP; ++p) sum += D1_PART(k, p, sl);
         int vi = -1;
         if (k == 0) {
-            if (sl < 4) vi = sl;
+            if (sl < 6) vi = sl;
         } else {
             const int col = 16 * (k - 1) + sl;
-            if (col < j) vi = 4 + col;
+            if (col < j) vi = 6 + col;
         }
         if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
     }
@@ -1592,7 +1596,7 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 // row sums, the 16 row totals summed in fixed order.
 __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent);
 // coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
-// RED_LAN: one-sweep Lanczos step (nv = 4 + j; 4 for factors without a Gram row; the last
+// RED_LAN: one-sweep Lanczos step (nv = 6 + j; 6 for factors without a Gram row; the last
 // block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
 __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
                                                    int coefJ, KArgs ax) {
@@ -1601,7 +1605,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     const DFac& d = F[blockIdx.y];
     const int c = blockIdx.x;
     const int nvs = nv;   // (the scalars' place after the values)
-    if (coefJ == RED_LAN && !d.track_gram) nv = 4;
+    if (coefJ == RED_LAN && !d.track_gram) nv = 6;
     if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
     const int npart = np > 0 ? np : d.npd;
@@ -1637,6 +1641,9 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         }
     }
     if (coefJ < 0 && coefJ != RED_LAN) return;
+    // (the one-sweep Lanczos' alpha estimate, read before the barrier: thread 0 of the last
+    // block overwrites it below)
+    const double al_est = coefJ == RED_LAN ? ld(d.sc, SC_ALPHA) : 0.0;
     __syncthreads();
     if (!last) return;
     auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1646,8 +1653,11 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         // the step's record row (as POST_LAN: H[j,j], H[j+1,j], btilde_j = <v_j,b>, the Gram
         // row of v_j) written through, with its host mirror, then the exchange / host signal
         const int j = ax.j, kmax = ax.kmax;
-        const double al = cld(0), uu = cld(1), vv = cld(2), bt = cld(3);
-        const double bsq = add_rn(sub_rn_(uu, mul_rn(2.0 * al, al)), mul_rn(mul_rn(al, al), vv));
+        const double al = cld(0), vv = cld(2), bt = cld(3), ww = cld(4), wv = cld(5);
+        // ||u - al v||^2 = ||wt + dl v||^2, wt = u - al' v, dl = al' - al (al' = alpha_{j-1},
+        // the estimate the sweep used): no cancellation of the size of alpha^2 (k_lan_1s)
+        const double dl = al_est - al;
+        const double bsq = add_rn(add_rn(ww, mul_rn(2.0 * dl, wv)), mul_rn(mul_rn(dl, dl), vv));
         const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
         const double ib = beta == 0.0 ? 0.0 : 1.0 / beta;
         if (t == 0) {
@@ -1664,7 +1674,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             double v = 0.0;
             if (i == j) v = al;
             else if (i == j + 1) v = beta;
-            else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? cld(4 + i - g0) : vv) : 0.0;
+            else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? cld(6 + i - g0) : vv) : 0.0;
             else if (i == rec_beta(kmax)) v = beta;
             else if (i == rec_bt(kmax)) v = bt;
             else if (i == rec_col(kmax)) v = (double)j;

@@ -222,6 +222,33 @@ def test_arnoldi_mid_run_flush(ctx, cls):
         assert np.array_equal(x, y) if exact else np.abs(x - y).max() <= 1e-12
 
 
+@pytest.mark.parametrize("shift", [1e4, 1e6])
+def test_lanczos_one_sweep_beta_with_large_shift(ctx, shift):
+    """the one-sweep Lanczos takes beta_j = ||u - alpha_j v_j|| from dots.  From |u|^2
+    (|u|^2 - 2 alpha^2 + alpha^2 |v|^2) it would lose eps (alpha/beta)^2 relative -- 1e-4 at
+    alpha/beta ~ 1e6; from u - alpha_{j-1} v_j (k_lan_1s, the previous alpha as estimate) it keeps
+    the reference's own accuracy (its vector u - alpha v carries eps alpha/beta relative).
+    tridiag(-1, 2 + shift, -1) (a Toeplitz band, the one-sweep kernels' storage)."""
+    tk = _tk()
+    n, K = 5000, 20
+    colptr, rowval, nz = tk.assemble_matrix(n, "Laplace")
+    nz = np.where(nz > 0, 2.0 + shift, -1.0)
+    csc = (colptr, rowval, nz)
+    bs = _rhs(n, 1, 13, distinct=True)
+    recs, _ = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K)
+    fo = O.Factor(csc, bs[0], K)
+    for j in range(1, K + 1):
+        fo.lanczos_ttr(j)
+    alpha = np.array([recs[j + 1][0, j] for j in range(K)])
+    beta = np.array([recs[j + 1][0, j + 1] for j in range(K)])
+    a_ref = np.array([fo.H[j, j] for j in range(K)])
+    b_ref = np.array([fo.H[j + 1, j] for j in range(K)])
+    assert np.all(a_ref / b_ref > shift / 10)                 # |alpha| >> beta
+    assert np.abs(alpha - a_ref).max() <= 1e-13 * np.abs(a_ref).max()
+    # each beta to its own magnitude (the reference's is good to ~eps * alpha / beta)
+    assert np.abs(beta / b_ref - 1).max() <= 1e-8, np.abs(beta / b_ref - 1).max()
+
+
 @pytest.mark.parametrize("ttr", ["auto", "ttr"])
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20),
                                      ("Laplace", 700, 75)])
