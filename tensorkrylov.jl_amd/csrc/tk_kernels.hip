@@ -718,16 +718,61 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2(const DFac* __r
         const double w = ld(d.W, r);
         const double u = ok ? (w - row_dot<MAXC, SC>(R, tv, toff, nc, h1)) : 0.0;
         st(d.U, r, u);
-        // factors sharing A_s: also the interleaved row the next step's k_spmv_mf gathers
-        // (the group's blocks of one tile range run on one XCD -- npart is a multiple of 8 --
-        // so its L2 merges their 8-byte pieces of each row)
-        if (d.Uint) st(d.Uint, r * ilv_pitch(d.inf) + d.ifs, u);
         reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
         const double e[2] = {u * u, vj * ld(d.b, r)};
         reduce_scalars<2>(e, tr, acc, nc, first);
         if (gram) reduce_row<MAXC>(R, tv, toff, nc, vj, tr, acc, nc + 2, first);
     }
     store_partials(acc, d.P2, a.npart, gram ? 2 * nc + 2 : nc + 2);
+}
+
+// k_arn_a2 for factors sharing one A_s (k_spmv_mf): each block walks its tiles for every
+// factor in turn -- the same per-factor arithmetic, partials and order -- and also writes the
+// tile's interleaved rows Uint[r][f] the next step's k_spmv_mf gathers, whole (256 rows x
+// pitch contiguous) from an LDS stage.  (8-byte stores of each factor's piece of every row
+// from the per-factor blocks cost pass 2 10-50 %; an interleaving pass of its own, 20 us.)
+template <int MAXC>
+__global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2_mf(const DFac* __restrict__ F, int nf, KArgs a) {
+    __shared__ double tr[CH * TSTR];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int j = a.j, nc = j + 1;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    const int pitch = ilv_pitch(nf);
+    const int ACC = (2 * nc + 2 + 15) & ~15;
+    double* stage = lds;                  // [f][row]
+    double* accb = lds + TPB * pitch;     // [f][ACC]
+    double* Ui = F[0].Uint;
+    bool first = true;
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += a.npart, first = false) {
+        const int64_t r = (int64_t)tile * TPB + threadIdx.x;
+        const bool ok = r < a.n;
+        const uint32_t toff = threadIdx.x * 16u;
+        for (int f = 0; f < nf; ++f) {
+            const DFac& d = F[f];
+            double* acc = accb + f * ACC;
+            const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(nc));
+            Row<MAXC> R;
+            R.load(tv, toff, nc);
+            const double vj = R.last;
+            const double w = ld(d.W, r);
+            const double u = ok ? (w - row_dot<MAXC, true>(R, tv, toff, nc, d.RED1)) : 0.0;
+            st(d.U, r, u);
+            stage[f * TPB + threadIdx.x] = u;
+            reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
+            const double e[2] = {u * u, vj * ld(d.b, r)};
+            reduce_scalars<2>(e, tr, acc, nc, first);
+            if (d.track_gram) reduce_row<MAXC>(R, tv, toff, nc, vj, tr, acc, nc + 2, first);
+        }
+        __syncthreads();
+        auto* out = GP(d2_t, Ui + (int64_t)tile * TPB * pitch);
+        for (int c = threadIdx.x; c < TPB * pitch / 2; c += TPB) {
+            const int e = 2 * c, row = e / pitch, col = e - row * pitch;
+            out[c] = (d2_t){col < nf ? stage[col * TPB + row] : 0.0, col + 1 < nf ? stage[(col + 1) * TPB + row] : 0.0};
+        }
+        __syncthreads();
+    }
+    for (int f = 0; f < nf; ++f)
+        store_partials(accb + f * ACC, F[f].P2, a.npart, F[f].track_gram ? 2 * nc + 2 : nc + 2);
 }
 
 // Write the pending column j+1 with no following step (U or W per a.ubuf: W after an
@@ -2355,8 +2400,16 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
         });
     });
 }
-void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
+void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s, bool mf) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
+    if (mf) {
+        const int nc = a.j + 1;
+        const size_t lds = ((size_t)TPB * ilv_pitch(nf) + (size_t)nf * ((2 * nc + 2 + 15) & ~15)) * sizeof(double);
+        with_maxc(nc, [&](auto M) {
+            hipLaunchKernelGGL((k_arn_a2_mf<decltype(M)::value>), dim3(a.npart, 1), dim3(TPB), lds, s, F, nf, a);
+        });
+        return;
+    }
     const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_a2<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);
