@@ -1351,7 +1351,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");
         }
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
-        RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s, dc->mfspmv), "arn_a2");
+        RUN(TCLS_PASS2, 2, launch_arn_a2(dc->df, nf, a, s), "arn_a2");
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 2, 2 * j + 4, dc->npart, s), "reduce");
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, ax, POST_ARN, fused ? 1 : 0, 1, s), "post");
         dc->pending = true;

@@ -133,9 +133,7 @@ void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
-// mf: factors sharing one A_s (k_spmv_mf): one block walks all factors of its tiles and also
-// writes the interleaved Uint rows
-void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s, bool mf = false);
+void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);

@@ -561,13 +561,38 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
 // The CGS2 first pass of factors sharing one A_s (the C3 gallery: five factors, one random
 // sparse matrix) is bound by its random gathers of U: ~15 distinct cache lines per row per
 // factor move from L2 to L1 for 8 useful bytes each.  With the factors' U rows interleaved
-// (Uint[r][f], written by k_arn_a2 beside U) one gather per nonzero fetches the entries of
+// (Uint[r][f], k_ilv) one gather per nonzero fetches the entries of
 // every factor, and k_spmv_mf writes each factor's A U with the same products and sums in the
 // same order as its own SpMV would (bitwise the same), which pass 1 then reads as one more
 // streamed vector.  F[0] carries the group's Uint (all factors' descriptors point to it).
 // Uint rows are padded to ilv_pitch(nf) doubles (a power of two: one aligned 16..64-byte
-// piece per row, read as 16-byte loads; the padding stays zero from the allocation).
+// piece per row, read as 16-byte loads).
 __host__ __device__ inline int ilv_pitch(int nf) { return nf <= 2 ? 2 : (nf <= 4 ? 4 : 8); }
+// One 256-row tile per block (ld_ is a multiple of 256): the factors' entries are transposed
+// through LDS so every wave store writes 1 KiB of contiguous Uint (row-strided 16-byte
+// stores left each line to be completed by four separate instructions; k_arn_a2 storing each
+// factor's 8-byte piece of every row cost that pass 10-50 %, one block walking all factors of
+// a tile cost it more)
+__global__ __launch_bounds__(TPB) void k_ilv(const DFac* __restrict__ F, int nf, int64_t ld_) {
+    __shared__ double tl[TPB * 9];   // row pitch 9: the transposing writes are conflict-free
+    const int64_t r0 = (int64_t)blockIdx.x * TPB;
+    const int t = threadIdx.x;
+    double* Ui = F[0].Uint;
+    const int p = ilv_pitch(nf);
+    double u[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f) u[f] = f < nf ? ld(F[f < nf ? f : 0].U, r0 + t) : 0.0;
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+        if (f < p) tl[t * 9 + f] = u[f];
+    __syncthreads();
+    const int nch = TPB * p / 2;   // 16-byte pieces of the tile's Uint rows
+    auto* out = GP(d2_t, Ui + r0 * p);
+    for (int c = t; c < nch; c += TPB) {
+        const int e = 2 * c, row = e / p, col = e - row * p;
+        out[c] = (d2_t){tl[row * 9 + col], tl[row * 9 + col + 1]};
+    }
+}
 // Four lanes per row (tools/gatherprobe.hip: one thread per row with three 16-byte gathers
 // per nonzero ran at 0.88 of the pattern's random-gather ceiling, four lanes at 0.98): lane p
 // of a row's quad gathers piece p (16 bytes, factors 2p and 2p+1) of the row's Uint entry, so a
@@ -724,55 +749,6 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2(const DFac* __r
         if (gram) reduce_row<MAXC>(R, tv, toff, nc, vj, tr, acc, nc + 2, first);
     }
     store_partials(acc, d.P2, a.npart, gram ? 2 * nc + 2 : nc + 2);
-}
-
-// k_arn_a2 for factors sharing one A_s (k_spmv_mf): each block walks its tiles for every
-// factor in turn -- the same per-factor arithmetic, partials and order -- and also writes the
-// tile's interleaved rows Uint[r][f] the next step's k_spmv_mf gathers, whole (256 rows x
-// pitch contiguous) from an LDS stage.  (8-byte stores of each factor's piece of every row
-// from the per-factor blocks cost pass 2 10-50 %; an interleaving pass of its own, 20 us.)
-template <int MAXC>
-__global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_a2_mf(const DFac* __restrict__ F, int nf, KArgs a) {
-    __shared__ double tr[CH * TSTR];
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int j = a.j, nc = j + 1;
-    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
-    const int pitch = ilv_pitch(nf);
-    const int ACC = (2 * nc + 2 + 15) & ~15;
-    double* stage = lds;                  // [f][row]
-    double* accb = lds + TPB * pitch;     // [f][ACC]
-    double* Ui = F[0].Uint;
-    bool first = true;
-    for (int tile = blockIdx.x; tile < a.ntiles; tile += a.npart, first = false) {
-        const int64_t r = (int64_t)tile * TPB + threadIdx.x;
-        const bool ok = r < a.n;
-        const uint32_t toff = threadIdx.x * 16u;
-        for (int f = 0; f < nf; ++f) {
-            const DFac& d = F[f];
-            double* acc = accb + f * ACC;
-            const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(nc));
-            Row<MAXC> R;
-            R.load(tv, toff, nc);
-            const double vj = R.last;
-            const double w = ld(d.W, r);
-            const double u = ok ? (w - row_dot<MAXC, true>(R, tv, toff, nc, d.RED1)) : 0.0;
-            st(d.U, r, u);
-            stage[f * TPB + threadIdx.x] = u;
-            reduce_row<MAXC>(R, tv, toff, nc, u, tr, acc, 0, first);
-            const double e[2] = {u * u, vj * ld(d.b, r)};
-            reduce_scalars<2>(e, tr, acc, nc, first);
-            if (d.track_gram) reduce_row<MAXC>(R, tv, toff, nc, vj, tr, acc, nc + 2, first);
-        }
-        __syncthreads();
-        auto* out = GP(d2_t, Ui + (int64_t)tile * TPB * pitch);
-        for (int c = threadIdx.x; c < TPB * pitch / 2; c += TPB) {
-            const int e = 2 * c, row = e / pitch, col = e - row * pitch;
-            out[c] = (d2_t){col < nf ? stage[col * TPB + row] : 0.0, col + 1 < nf ? stage[(col + 1) * TPB + row] : 0.0};
-        }
-        __syncthreads();
-    }
-    for (int f = 0; f < nf; ++f)
-        store_partials(accb + f * ACC, F[f].P2, a.npart, F[f].track_gram ? 2 * nc + 2 : nc + 2);
 }
 
 // Write the pending column j+1 with no following step (U or W per a.ubuf: W after an
@@ -2373,7 +2349,7 @@ void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 }
 void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
-    // (Uint is written by the previous step's k_arn_a2: no interleaving pass)
+    hipLaunchKernelGGL(k_ilv, dim3((int)(a.ld / TPB)), dim3(TPB), 0, s, F, nf, a.ld);
     const int nb = (int)((a.ld + TPB / 4 - 1) / (TPB / 4));
     auto go = [&](auto FM) {
         constexpr int FMv = decltype(FM)::value;
@@ -2400,16 +2376,8 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
         });
     });
 }
-void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s, bool mf) {
+void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
-    if (mf) {
-        const int nc = a.j + 1;
-        const size_t lds = ((size_t)TPB * ilv_pitch(nf) + (size_t)nf * ((2 * nc + 2 + 15) & ~15)) * sizeof(double);
-        with_maxc(nc, [&](auto M) {
-            hipLaunchKernelGGL((k_arn_a2_mf<decltype(M)::value>), dim3(a.npart, 1), dim3(TPB), lds, s, F, nf, a);
-        });
-        return;
-    }
     const size_t lds = lds_bytes(2 * a.j + 4, a.kmax, TK_A2_SCALAR ? 0 : 1);
     with_maxc(a.j + 1, [&](auto M) {
         hipLaunchKernelGGL((k_arn_a2<decltype(M)::value>), dim3(a.npart, nf), dim3(TPB), lds, s, F, a);

@@ -478,7 +478,7 @@ def test_fused_flush_basis_mul_identical(ctx, cls, n, t, method, monkeypatch):
 @pytest.mark.parametrize("nf,csr", [(5, False), (3, True), (2, False), (8, False)])
 def test_shared_matrix_spmv_bitwise(ctx, nf, csr, monkeypatch):
     """CGS2 factors that share one gather-format A_s take A U from one interleaved gather per
-    nonzero (Uint written by k_arn_a2, gathered by k_spmv_mf): records and bases bitwise those of the per-factor SpMV
+    nonzero (k_ilv + k_spmv_mf, four lanes per row): records and bases bitwise those of the per-factor SpMV
     (TKHIP_MFSPMV=0), SELL-256 and CSR storage."""
     tk = _tk()
     n, K = 4000, 24
