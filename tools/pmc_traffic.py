@@ -15,6 +15,7 @@ import os
 import sys
 
 STEP_KERNELS = ("k_arn_a1", "k_arn_a2", "k_arn_d1", "k_reduce", "k_post", "k_lan_", "k_spmv_mf", "k_ilv")
+GATHER_KERNELS = ("k_spmv_mf",)
 
 
 def load(d, counter):
@@ -36,11 +37,15 @@ def main():
     ff = float(os.environ.get("FETCH_FACTOR", "2"))
     fetch = load(fdir, "FETCH_SIZE")
     write = load(wdir, "WRITE_SIZE")
-    step_f = sum(v for k, v in fetch.items() if any(s in k for s in STEP_KERNELS))
+    # the doubling applies to wide streaming reads; k_spmv_mf's random 64-byte gathers are
+    # tallied at their size (raw FETCH_SIZE = 64 B x nonzeros at C3)
+    step_f = sum(v * (1.0 / ff if any(g in k for g in GATHER_KERNELS) else 1.0)
+                 for k, v in fetch.items() if any(s in k for s in STEP_KERNELS))
     step_w = sum(v for k, v in write.items() if any(s in k for s in STEP_KERNELS))
     per_kernel = {k: {"fetch_KiB": fetch.get(k, 0.0), "write_KiB": write.get(k, 0.0)}
                   for k in sorted(set(fetch) | set(write))}
     res = {"config": cfg, "n_gpus": int(ngpu), "K": K, "fetch_factor": ff,
+           "fetch_factor_note": "x%g on streaming reads; x1 on the random 64-B gathers of %s" % (ff, GATHER_KERNELS),
            "hbm_bytes_per_step": (ff * step_f + step_w) * 1024.0 / K,
            "fetch_bytes_per_step_raw": step_f * 1024.0 / K, "write_bytes_per_step": step_w * 1024.0 / K,
            "per_kernel_KiB": per_kernel}
