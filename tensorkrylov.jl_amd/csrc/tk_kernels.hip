@@ -2008,8 +2008,10 @@ __global__ __launch_bounds__(TPB) void k_post(const DFac* __restrict__ F, KArgs 
                 const double vav = ld(d.RED1, 2);
                 st(d.g, 0, vav);
                 st(d.sc, SC_INVBETA, 1.0);
-                st(d.sc, SC_ALPHA, 0.0);      // (one-sweep Lanczos step 0: v_0 = 1 .* (U - 0 * 0),
-                st(d.sc, SC_BETAPREV, 0.0);   //  u_0 = A v_0 - 0 * 0)
+                // one-sweep Lanczos step 0: v_0 = 1 .* (U - alpha * 0), u_0 = A v_0 - 0 * 0; alpha
+                // is only the estimate of alpha_0 = <v0, A v0> its beta is taken around (k_lan_1s)
+                st(d.sc, SC_ALPHA, vav);
+                st(d.sc, SC_BETAPREV, 0.0);
                 double* o = d.RED1 + 2;   // (k_arn_d1 step 0 reads its scalars here)
                 st(o, D1S_IB, 1.0);
                 st(o, D1S_GAMMA, vav);
