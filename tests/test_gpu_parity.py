@@ -243,8 +243,11 @@ def test_lanczos_one_sweep_beta_with_large_shift(ctx, shift):
     beta = np.array([recs[j + 1][0, j + 1] for j in range(K)])
     a_ref = np.array([fo.H[j, j] for j in range(K)])
     b_ref = np.array([fo.H[j + 1, j] for j in range(K)])
-    assert np.all(a_ref / b_ref > shift / 10)                 # |alpha| >> beta
-    assert np.abs(alpha - a_ref).max() <= 1e-13 * np.abs(a_ref).max()
+    ratio = (a_ref / b_ref).min()
+    assert ratio > shift / 10                                 # |alpha| >> beta
+    # alpha: two correct implementations differ within the problem's own conditioning,
+    # eps * alpha / beta relative (v_j carries it)
+    assert np.abs(alpha / a_ref - 1).max() <= max(1e-13, 1e-14 * ratio), np.abs(alpha / a_ref - 1).max()
     # each beta to its own magnitude (the reference's is good to ~eps * alpha / beta)
     assert np.abs(beta / b_ref - 1).max() <= 1e-8, np.abs(beta / b_ref - 1).max()
 
