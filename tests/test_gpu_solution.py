@@ -67,10 +67,12 @@ def test_returned_solution_matches_oracle_and_solves_the_system(ctx, cls, method
     assert all(r >= tol for r in conv.relative_residual_norm[1:k - 1])
     lam_o, X_o = x_o
     t = len(lam_o)
-    # LanczosReorth converges here at k = 28 of n = 30, next to the full Krylov space, with
-    # MGS redos taken at loss ~ sqrt(eps): its basis agrees with the oracle's to ~1e-12 relative
-    # (test_gpu_parity follows the redo decisions at 1e-7), the other methods to 1e-13
-    xtol = 1e-10 if method == "TensorLanczosReorth" else 1e-12
+    # The Lanczos methods converge here at k = 28 of n = 30, next to the full Krylov space: plain
+    # TTR has lost orthogonality there and amplifies rounding differences (reduction order, the
+    # one-sweep beta formula), LanczosReorth takes MGS redos at loss ~ sqrt(eps) (test_gpu_parity
+    # follows its decisions at 1e-7): their X agree with the oracle's to ~1e-12 relative, Arnoldi's
+    # to 1e-13
+    xtol = 1e-10 if method in ("TensorLanczos", "TensorLanczosReorth") else 1e-12
     # lambda and the factor matrices (basis_tensor_mul! on the device) vs the oracle
     assert x.ncomponents() == t and x.ndims() == d
     assert np.abs(x.lam - lam_o).max() <= 1e-12 * np.abs(lam_o).max()
