@@ -381,6 +381,14 @@ def main():
                 "engine": ("k_fin_vy: flush of the pending column + V*Y from its register row (FP64 FMA), "
                            "one read of V" if fused_vy else "k_basis_mul (MFMA) after the flush"),
                 "avg_us": round(vy_s * 1e6, 2),
+                "GB_s": round((vy_bytes + 8 * n * part.nf) / vy_s / 1e9, 1) if vy_cnt else None,
+                **({"why_fma": "V*Y at t=%d, k=%d is %.1f flop/B, below the fp64 ridge (78.6 TF / 8 TB/s = 9.8): "
+                               "HBM-bound either way, and on gfx950 fp64 MFMA and fp64 VALU FMA have the same "
+                               "peak (78.6 TF); the fused kernel reads V once for the flush and the product "
+                               "(the MFMA kernel, basis_mul_mfma, needs the column flushed first: a second read "
+                               "of V).  Both run at 94-96 %% of the measured ceiling of this read/write mix "
+                               "(profiles/r02/rwprobe_c2_vy_ceiling.txt, 779 us at C2)"
+                               % (t_loc, K, vy_flops / vy_bytes)} if fused_vy else {}),
             },
             "orthogonality_gram": ({"mode": "deferred: one v_mfma_f64_16x16x4f64 SYRK of factor 1's basis "
                                             "per solve (tk_decomp_gram)",

@@ -1656,6 +1656,15 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             // one-sweep step: publish the value coherently (agent-scope store, through to the
             // device-coherent level; its completion awaited), then count the arrival -- no
             // L2 writeback.  The last of the nv blocks of this factor evaluates the scalars.
+            // This is the hand-off row "ONE lane of each storing workgroup ... an agent-scope
+            // atomic add | ... the workgroup whose add came last, told by the value its add
+            // returned | ... the other waves load after a workgroup barrier" of the measured
+            // table in /opt/skills/guides/MI355X_MICROARCH.md (stores and loads sc1 = the
+            // agent-scope relaxed atomics here, vmcnt(0) before the add): measured correct on
+            // gfx950, not an architectural guarantee.  The memory-model form -- a
+            // release on the add, an acquire in the last block -- writes back / invalidates L2
+            // on this 8-XCD part: 5x slower pass kernels when tried.  ctr's reset
+            // below is ordered before the next launch by the kernel boundary.
             __hip_atomic_store(d.RED1 + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_s_waitcnt(0);
             last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
