@@ -653,6 +653,7 @@ struct tk_decomp {
     // of its basis when asked (tk_decomp_gram) instead of a Gram row per step (TKHIP_GRAM)
     bool gram_deferred = false;
     double* gram_scr = nullptr;
+    bool gram_scr_owned_by_allocs = false;   // (allocated at create: freed with allocs)
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -722,7 +723,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->scratch) hipFree(dc->scratch);
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
-    if (dc->gram_scr) hipFree(dc->gram_scr);
+    if (dc->gram_scr && !dc->gram_scr_owned_by_allocs) hipFree(dc->gram_scr);
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
@@ -881,6 +882,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
     }
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+    // the deferred Gram's partials (tk_decomp_gram), allocated with the rest: an allocation at
+    // the first call cost up to ~15 ms inside the driver loop
+    if (dc->gram_deferred && nf > 0) {
+        DA(dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double));
+        dc->gram_scr_owned_by_allocs = true;
+    }
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
     if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);

@@ -149,16 +149,17 @@ def _fill_deferred_orthogonality(conv, td, k_last):
     owning factor 1 computes them and one all-reduce (every rank calls it here) shares them."""
     if not _gram_deferred(td) or k_last < 2:
         return
-    from .compressed import orthogonality_loss_from_gram
+    from .compressed import orthogonality_losses_from_gram
+    t0 = time.perf_counter()
     part = td.part
     orth = np.zeros(k_last)
     if part.first == 0 and part.nf > 0 and not part.replica:
         G = td.dev.gram(0, k_last)
-        for k in range(2, k_last + 1):
-            orth[k - 1] = orthogonality_loss_from_gram(G, k)
+        orth[:] = orthogonality_losses_from_gram(G)
     if part.nranks > 1:
         orth = td.ctx.allreduce_host(orth)
     conv.orthogonality_data[1:k_last] = orth[1:k_last]
+    conv.timing["orth_gram_s"] = time.perf_counter() - t0
 
 
 def _solution(td, k, lam, Ys):

@@ -447,3 +447,16 @@ def test_solution_host_logic(cls, method, tol):
         vecb = np.kron(vecb, b[s])
     res = np.linalg.norm(tkamd.kronecker_sum_matvec(A, tkamd.kroneckervectorize(x)) - vecb)
     assert abs(res - conv.relative_residual_norm[k - 1]) <= 1e-6 * conv.relative_residual_norm[k - 1]
+
+
+def test_orthogonality_losses_from_one_gram():
+    """orthogonality_data from one Gram matrix (deferred Gram, tk_decomp_gram): every prefix
+    loss norm(G[:k,:k] - I) (src/orthogonal_bases.jl:250-257) equals the per-k form."""
+    from tkamd.compressed import orthogonality_loss_from_gram, orthogonality_losses_from_gram
+    rng = np.random.default_rng(0)
+    V = np.linalg.qr(rng.standard_normal((500, 40)))[0] + 1e-13 * rng.standard_normal((500, 40))
+    G = V.T @ V
+    a = orthogonality_losses_from_gram(G)
+    b = np.array([orthogonality_loss_from_gram(G, k) for k in range(1, 41)])
+    assert np.allclose(a, b, rtol=1e-12, atol=0)
+    assert np.allclose(a, [np.linalg.norm(V[:, :k].T @ V[:, :k] - np.eye(k)) for k in range(1, 41)], rtol=1e-6)
