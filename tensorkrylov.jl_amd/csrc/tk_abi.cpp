@@ -654,6 +654,8 @@ struct tk_decomp {
     bool gram_deferred = false;
     double* gram_scr = nullptr;
     bool gram_scr_owned_by_allocs = false;   // (allocated at create: freed with allocs)
+    double* gram_host = nullptr;             // pinned readback of the Gram values (a first D2H
+                                             // copy into pageable memory cost ~9 ms)
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -724,6 +726,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->Ydev) hipFree(dc->Ydev);
     if (dc->Xdev) hipFree(dc->Xdev);
     if (dc->gram_scr && !dc->gram_scr_owned_by_allocs) hipFree(dc->gram_scr);
+    if (dc->gram_host) hipHostFree(dc->gram_host);
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
@@ -887,6 +890,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     if (dc->gram_deferred && nf > 0) {
         DA(dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double));
         dc->gram_scr_owned_by_allocs = true;
+        void* hp = nullptr;
+        if (hipHostMalloc(&hp, (size_t)gram_values(64) * sizeof(double), hipHostMallocDefault) == hipSuccess)
+            dc->gram_host = (double*)hp;
+        (void)hipGetLastError();
     }
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
@@ -1675,8 +1682,13 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     LAUNCHCHK("gram");
     if (!G) return TK_OK;
     const int nv = gram_values(k);
-    std::vector<double> v(nv);
-    HIPCHK(hipMemcpyAsync(v.data(), dc->gram_scr + gram_result_offset(dc->ntiles, k), nv * sizeof(double),
+    std::vector<double> vbuf;
+    double* v = dc->gram_host;
+    if (!v) {
+        vbuf.resize(nv);
+        v = vbuf.data();
+    }
+    HIPCHK(hipMemcpyAsync(v, dc->gram_scr + gram_result_offset(dc->ntiles, k), nv * sizeof(double),
                           hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     // k_gram's layout: group pair i (ga <= gb), register r, lane l -> G[col(ga, m), col(gb, n)]
