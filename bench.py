@@ -285,6 +285,7 @@ def main():
                **({"relres_bitwise_equal_to_n1": bool(np.array_equal(conv.relative_residual_norm, ref_relres))}
                   if ref_relres is not None else {}),
                "host_threads": tkamd.solver._native_threads(),
+               "phases_s": {k_: round(v_, 6) for k_, v_ in conv.timing.items()},
                "final_relative_residual": float(conv.relative_residual_norm[conv.niterations - 1]),
                "note": "tkamd.tensorkrylov (src/tensor_krylov_method.jl:36-125) iterations k = 2..K: "
                        "device steps enqueued ahead + the native host loop (tk_solver_run: records "

@@ -654,8 +654,12 @@ struct tk_decomp {
     bool gram_deferred = false;
     double* gram_scr = nullptr;
     bool gram_scr_owned_by_allocs = false;   // (allocated at create: freed with allocs)
-    double* gram_host = nullptr;             // pinned readback of the Gram values (a first D2H
-                                             // copy into pageable memory cost ~9 ms)
+    // the Gram values land in host-mapped memory, then a sequence word (k_mirror_records, as
+    // the records): the host spins on the word instead of a copy + stream sync (that path
+    // cost ~7-9 ms at its first use in a process, inside the driver loop)
+    double* gram_host = nullptr;
+    unsigned long long* gram_done = nullptr;
+    unsigned long long gram_seq = 0;
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -727,6 +731,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->Xdev) hipFree(dc->Xdev);
     if (dc->gram_scr && !dc->gram_scr_owned_by_allocs) hipFree(dc->gram_scr);
     if (dc->gram_host) hipHostFree(dc->gram_host);
+    if (dc->gram_done) hipHostFree(dc->gram_done);
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
@@ -891,8 +896,17 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double));
         dc->gram_scr_owned_by_allocs = true;
         void* hp = nullptr;
-        if (hipHostMalloc(&hp, (size_t)gram_values(64) * sizeof(double), hipHostMallocDefault) == hipSuccess)
+        void* hd = nullptr;
+        if (hipHostMalloc(&hp, (size_t)gram_values(64) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) ==
+                hipSuccess &&
+            hipHostMalloc(&hd, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
             dc->gram_host = (double*)hp;
+            dc->gram_done = (unsigned long long*)hd;
+            *dc->gram_done = 0;
+        } else {
+            if (hp) hipHostFree(hp);
+            if (hd) hipHostFree(hd);
+        }
         (void)hipGetLastError();
     }
     // records go through the RCCL exchange whenever factors are spread over ranks;
@@ -1683,14 +1697,30 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     if (!G) return TK_OK;
     const int nv = gram_values(k);
     std::vector<double> vbuf;
-    double* v = dc->gram_host;
-    if (!v) {
+    const double* v = dc->gram_host;
+    const double* res = dc->gram_scr + gram_result_offset(dc->ntiles, k);
+    if (v) {
+        const unsigned long long want = ++dc->gram_seq;
+        launch_mirror_records(res, dc->gram_host, nv, dc->gram_done, 1, want, s);
+        LAUNCHCHK("gram mirror");
+        long spins = 0;
+        Deadline dl;
+        while (__atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want) {
+            if (++spins % 4096 == 0) {
+                hipError_t e = hipStreamQuery(s);
+                if (e != hipSuccess && e != hipErrorNotReady)
+                    return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
+                if (e == hipSuccess && __atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want)
+                    return fail(TK_ERR_STATE, "tk_decomp_gram: the result never arrived");
+                if (dl.elapsed() > dl.lim) return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
+            }
+        }
+    } else {
         vbuf.resize(nv);
+        HIPCHK(hipMemcpyAsync(vbuf.data(), res, nv * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
         v = vbuf.data();
     }
-    HIPCHK(hipMemcpyAsync(v, dc->gram_scr + gram_result_offset(dc->ntiles, k), nv * sizeof(double),
-                          hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
     // k_gram's layout: group pair i (ga <= gb), register r, lane l -> G[col(ga, m), col(gb, n)]
     // with m = (l>>4) + 4r, n = l&15, col(g, x) = 32 (g>>1) + 2x + (g&1)
     const int ngr = k <= 32 ? 2 : 4;
