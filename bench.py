@@ -184,9 +184,11 @@ def main():
         dev.sweep(0, K)                 # enqueues K steps; returns before they run
         host_issue[0] += time.perf_counter() - h0
         host_issue[1] += 1
-        dev.basis_mul(K, Ys, want=False)   # finalizes the pending column V[:, K] first (fused for Arnoldi)
         if gram_owner:
-            dev.gram(0, K, want=False)      # orthogonality_data for k = 2..K from one Gram
+            # orthogonality_data for k = 2..K from one Gram of V[:, :K] (its own stream: it
+            # overlaps the flush + V*Y below, which writes column K only)
+            dev.gram(0, K, want=False)
+        dev.basis_mul(K, Ys, want=False)   # finalizes the pending column V[:, K] first (fused for Arnoldi)
 
     def barrier():
         ctx.sync()

@@ -77,6 +77,7 @@ struct tk_ctx {
     int device = 0;
     hipStream_t stream = nullptr;    // compute
     hipStream_t xstream = nullptr;   // per-step record exchange (RCCL), overlaps compute
+    hipStream_t gstream = nullptr;   // deferred orthogonality Gram (tk_decomp_gram), overlaps compute
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     int timing = 0;   // 0 off, 1 step level, 2 per kernel class
@@ -230,6 +231,7 @@ tk_status tk_ctx_create(int device, tk_ctx** out) { TK_API_BEGIN
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->xstream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
         return fail(TK_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -244,6 +246,7 @@ static void ctx_release(tk_ctx* c) {
     hipSetDevice(c->device);
     if (!c->stuck) sync_bounded(c, c->stream, "tk_ctx_destroy");
     if (!c->stuck) sync_bounded(c, c->xstream, "tk_ctx_destroy");
+    if (!c->stuck) sync_bounded(c, c->gstream, "tk_ctx_destroy");
     if (c->stuck) return;   // a collective may still run: its resources are left to process exit
     drain_timers(c);
     for (hipEvent_t e : c->evpool) hipEventDestroy(e);
@@ -251,6 +254,7 @@ static void ctx_release(tk_ctx* c) {
     if (c->xbuf) hipFree(c->xbuf);
     hipStreamDestroy(c->stream);
     hipStreamDestroy(c->xstream);
+    hipStreamDestroy(c->gstream);
     delete c;
 }
 
@@ -266,6 +270,7 @@ tk_status tk_ctx_sync(tk_ctx* c) { TK_API_BEGIN
     HIPCHK(hipSetDevice(c->device));
     STUCKCHK(c);
     tk_status st = sync_bounded(c, c->stream, "tk_ctx_sync (compute stream)");
+    if (st == TK_OK) st = sync_bounded(c, c->gstream, "tk_ctx_sync (Gram stream)");
     return st ? st : sync_bounded(c, c->xstream, "tk_ctx_sync (exchange stream)");
     TK_API_END
 }
@@ -660,6 +665,11 @@ struct tk_decomp {
     double* gram_host = nullptr;
     unsigned long long* gram_done = nullptr;
     unsigned long long gram_seq = 0;
+    // the SYRK runs on a stream of its own (it only reads finished columns), so it overlaps
+    // what the caller enqueues next -- the flush + V*Y of the solve's end; a new sequence
+    // (tk_decomp_init) waits for it before rewriting the basis
+    hipEvent_t gev_in = nullptr, gev_done = nullptr;   // (the context's Gram stream)
+    bool gram_inflight = false;
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -738,6 +748,8 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->hdone) hipHostFree(dc->hdone);
     if (dc->xdone) hipHostFree(dc->xdone);
     if (dc->cstream) hipStreamDestroy(dc->cstream);
+    if (dc->gev_in) hipEventDestroy(dc->gev_in);
+    if (dc->gev_done) hipEventDestroy(dc->gev_done);
     delete dc;
 }
 
@@ -895,6 +907,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     if (dc->gram_deferred && nf > 0) {
         DA(dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double));
         dc->gram_scr_owned_by_allocs = true;
+        if (hipEventCreateWithFlags(&dc->gev_in, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+            hipEventCreateWithFlags(&dc->gev_done, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+            free_decomp(dc);
+            return fail(TK_ERR_HIP, "tk_decomp_create: gram stream / events");
+        }
         void* hp = nullptr;
         void* hd = nullptr;
         if (hipHostMalloc(&hp, (size_t)gram_values(64) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) ==
@@ -1092,6 +1109,7 @@ tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     // waited for with the deadline.
     if (!c->stuck) sync_bounded(c, c->stream, "tk_decomp_destroy (compute stream)");
     if (!c->stuck) sync_bounded(c, c->xstream, "tk_decomp_destroy (exchange stream)");
+    if (!c->stuck) sync_bounded(c, c->gstream, "tk_decomp_destroy (Gram stream)");
     free_decomp(dc);
     for (tk_mat* A : mats) mat_release(A);
     ctx_release(c);
@@ -1247,6 +1265,10 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     tk_status st = dc->failed ? TK_OK : bk_flush(dc);
     if (st) return st;
     dc->bk_j = -1;
+    if (dc->gram_inflight) {   // (a Gram of the previous sequence still reads the basis)
+        HIPCHK(hipStreamWaitEvent(s, dc->gev_done, 0));
+        dc->gram_inflight = false;
+    }
     st = slot_guard(dc, 0);
     if (st) return st;
     KArgs a = base_args(dc, 0, 0);
@@ -1687,13 +1709,20 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         if (st) return st;
     }
     if (!dc->gram_scr) HIPCHK(hipMalloc((void**)&dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double)));
-    hipStream_t s = c->stream;
+    // on the Gram stream after everything enqueued so far (the steps that wrote columns < k)
+    hipStream_t s = c->gstream;
     {
-        Timer tm(c, TCLS_GRAM, 1);
+        HIPCHK(hipEventRecord(dc->gev_in, c->stream));
+        HIPCHK(hipStreamWaitEvent(s, dc->gev_in, 0));
+    }
+    {
+        Timer tm(c, TCLS_GRAM, 1, s);
         KArgs a = base_args(dc, 0, 0);
         launch_gram(dc->df, f, a, k, dc->gram_scr, s);
     }
     LAUNCHCHK("gram");
+    HIPCHK(hipEventRecord(dc->gev_done, s));
+    dc->gram_inflight = true;
     if (!G) return TK_OK;
     const int nv = gram_values(k);
     std::vector<double> vbuf;
