@@ -184,11 +184,11 @@ def main():
         dev.sweep(0, K)                 # enqueues K steps; returns before they run
         host_issue[0] += time.perf_counter() - h0
         host_issue[1] += 1
-        if gram_owner:
-            # orthogonality_data for k = 2..K from one Gram of V[:, :K] (its own stream: it
-            # overlaps the flush + V*Y below, which writes column K only)
-            dev.gram(0, K, want=False)
         dev.basis_mul(K, Ys, want=False)   # finalizes the pending column V[:, K] first (fused for Arnoldi)
+        if gram_owner:
+            # orthogonality_data for k = 2..K from one Gram of V[:, :K] (after the V*Y: run
+            # beside it, the two kernels took longer together than one after the other)
+            dev.gram(0, K, want=False)
 
     def barrier():
         ctx.sync()

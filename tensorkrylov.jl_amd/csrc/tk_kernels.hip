@@ -2217,6 +2217,9 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
 // col(g, i) = 32 (g>>1) + 2i + (g&1).  Blocks walk tiles (tile += gridDim.x, the grid a
 // function of n only); the 4 waves' accumulators are summed in fixed order through LDS and
 // each block writes its partial Pg[block][value]; k_gram_reduce sums partials in block order.
+#ifndef TK_GRAM_GQ
+#define TK_GRAM_GQ 8   // row quads whose loads are in flight before their MFMAs
+#endif
 template <int NBLK>
 __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs a, int f, int k,
                                               double* __restrict__ Pg) {
@@ -2234,7 +2237,7 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
         const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(k));
         // GQ row quads' loads in flight before their MFMAs (pairs past k read 0; the odd
         // column k of the last pair is stale and masked)
-        constexpr int GQ = 8;
+        constexpr int GQ = TK_GRAM_GQ;
 #pragma unroll 1
         for (int q0 = 0; q0 < 16; q0 += GQ) {
             d2_t x[GQ][NBLK];
