@@ -76,8 +76,10 @@ def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None, 
     if method == "TensorArnoldi":
         return mb + vec + 2 * 8 * n * k + 8 * n + 8 * n
     if method == "TensorLanczos" and sweeps == 1:
-        # one-sweep TTR (k_lan_1s): u_{k-1} and v_{k-1} read, v_k and u_k written, <v_k, b>;
-        # the SpMV takes v_k from LDS (+ the tracked factor's Gram row, gram_bytes_step)
+        # one-sweep TTR (k_lan_1w / k_lan_1s): u_{k-1} and v_{k-1} read, v_k and u_k written,
+        # <v_k, b>; the SpMV takes v_k from LDS (+ the tracked factor's Gram row,
+        # gram_bytes_step).  Not counted: the paired-column layout's half (v_{k-1} read from
+        # its pair after an even step, rewritten with v_k after an odd one), 8n per step
         return 5 * 8 * n + mb
     b = mb + vec + 8 * n + 8 * n + 8 * n
     if method == "TensorLanczosReorth":

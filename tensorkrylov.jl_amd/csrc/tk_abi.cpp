@@ -642,6 +642,7 @@ struct tk_decomp {
     bool onesweep = false;  // Arnoldi as one sweep per step (k_arn_d1): banded A_s only
     bool fin_d = true;      // ungated column writes through k_fin_d (TKHIP_FIN_D=0: tile-loop kernels)
     int npd = 0;            // max DFac::npd over the local factors (grid width of k_arn_d1)
+    int nwl = 0;            // max DFac::nwl (grid width of k_lan_1w)
     bool inited = false;
     bool pending = false;   // last step's column j+1 not yet written (fused pipeline)
     bool in_sweep = false;  // inside tk_decomp_sweep: one timing pair for the whole sweep
@@ -657,6 +658,7 @@ struct tk_decomp {
     // orthogonality_data of global factor 0 (src/tensor_krylov_method.jl:103) from one MFMA SYRK
     // of its basis when asked (tk_decomp_gram) instead of a Gram row per step (TKHIP_GRAM)
     bool gram_deferred = false;
+    bool any_gram = false;   // some local factor keeps a per-step Gram row
     double* gram_scr = nullptr;
     bool gram_scr_owned_by_allocs = false;   // (allocated at create: freed with allocs)
     // the Gram values land in host-mapped memory, then a sequence word (k_mirror_records, as
@@ -863,6 +865,8 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             d.npd = wpb >= 1 ? (d.nwin + wpb - 1) / wpb : (d.nwin + std::max(1, d.nwin / npcap) - 1) / std::max(1, d.nwin / npcap);
         }
         dc->npd = std::max(dc->npd, d.npd);
+        d.nwl = lan_windows(n, d.hl, d.hu);
+        dc->nwl = std::max(dc->nwl, d.nwl);
         const int npp = std::max(std::max(dc->npart, dc->onesweep ? d.npd : 0), dc->ntiles);
         DA(d.V, (size_t)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double));   // tile-major, paired columns
         double* bb;
@@ -885,6 +889,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram == 1 || method == TK_LANCZOS_REORTH || (gi == 0 && !dc->gram_deferred)) ? 1 : 0;
+        dc->any_gram = dc->any_gram || d.track_gram;
         d.gidx = gi;
         d.Uint = nullptr;
         d.AU = nullptr;
@@ -1409,8 +1414,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // one sweep: writes v_j (E or its pair) and u_j; the reduce's last block takes
         // alpha_j, beta_j and writes the step's record (no post launch)
         a.ubuf = j & 1;
-        RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->npd, s), "lan_1s");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, 0, s, 0, RED_LAN, &ax), "reduce");
+        // (no Gram row: k_lan_1w's wide windows, DFac::nwl partials -- np -1 to the reduce)
+        RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->any_gram ? dc->npd : dc->nwl, dc->any_gram, s), "lan_1s");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, dc->any_gram ? 0 : -1, s, 0, RED_LAN, &ax), "reduce");
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;

@@ -65,6 +65,9 @@ struct DFac {
     // row windows of stride 256 - 2(hl+hu), window count, partial blocks (a function of
     // n, hl, hu only)
     int hl, hu, nwin, npd;
+    // one-sweep Lanczos without a Gram row (k_lan_1w): windows of LAN_RPT * 256 rows owning
+    // all but hl + hu of them (one SpMV), their count (a function of n, hl, hu only)
+    int nwl;
     // one-sweep Arnoldi: the even column written by the last even step (v_j, n rows); the
     // odd step after it stores the pair (v_{j-1}, v_j) once, so no column is written twice
     double* E;
@@ -137,7 +140,17 @@ void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
-void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, bool gram, hipStream_t s);
+// rows per thread of k_lan_1w (its windows are LAN_RPT * 256 rows; 2: 67 us per C2 step
+// against 71 at 4 and 77 at 8, profiles/r03/lan_rpt_ab.txt)
+#ifndef TK_LAN_RPT
+#define TK_LAN_RPT 2
+#endif
+constexpr int LAN_RPT = TK_LAN_RPT;
+inline int lan_windows(int64_t n, int hl, int hu) {
+    const int ws = LAN_RPT * 256 - hl - hu;
+    return (int)((n + ws - 1) / ws);
+}
 void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_lan_l1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);

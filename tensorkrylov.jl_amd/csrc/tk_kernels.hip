@@ -45,8 +45,9 @@ namespace tk {
 // allow; these limits are the largest that compile without spills.
 #define OCC_WAVES(L4, L3) (MAXC <= (L4) ? 4 : (MAXC <= (L3) ? 3 : 2))
 // SpMV-fused kernels: the gather formats need more registers
-#define A1_L4(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 40 : ((F) == 2 ? 24 : 16))
-#define A1_L3(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 56 : ((F) == 2 ? 40 : 32))
+// (6 = SPM_PRE: no gathers, the register budget of the second pass)
+#define A1_L4(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 40 : ((F) == 2 ? 24 : ((F) == 6 ? 32 : 16)))
+#define A1_L3(F) ((F) == 1 || (F) == 3 || (F) == 4 || (F) == 5 ? 56 : ((F) == 2 ? 40 : ((F) == 6 ? 48 : 32)))
 #define OCC_ATTR(L4, L3) __attribute__((amdgpu_waves_per_eu(OCC_WAVES(L4, L3), OCC_WAVES(L4, L3))))
 #ifndef TK_A1_SCALAR
 #define TK_A1_SCALAR 1
@@ -456,7 +457,8 @@ __device__ __forceinline__ void st_x(double* p, int64_t i, double v) {
 // separately rounded (Julia's CSC scatter order).  x(c) supplies the vector entry.
 // FMT: SPM_DIA / SPM_SELL / SPM_CSR fixes the storage at compile time (fewer live
 // registers in the fused kernels); SPM_ANY decides at run time.
-enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3, SPM_DIAN = 4, SPM_DIAT = 5 };
+enum { SPM_ANY = 0, SPM_DIA = 1, SPM_SELL = 2, SPM_CSR = 3, SPM_DIAN = 4, SPM_DIAT = 5,
+       SPM_PRE = 6 };   // SPM_PRE: CGS2 pass 1 reads A U from DFac::AU (k_spmv_mf ran), no SpMV
 template <int FMT, class XF>
 __device__ __forceinline__ double spmv(const SpM& A, int64_t r, XF x) {
 #pragma clang fp contract(off)
@@ -705,7 +707,9 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
         Row<MAXC> R;
         R.load(tv, toff, j);
         const double* Ug = d.U;
-        const double au = !ok ? 0.0 : (a.mfs ? ld(d.AU, r) : spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }));
+        double au = 0.0;
+        if constexpr (FMT == SPM_PRE) au = ok ? ld(d.AU, r) : 0.0;
+        else au = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Ug, c); }) : 0.0;
         const double up = ld(d.U, r);
         const double vj = ok ? (up - row_dot<MAXC, SC>(R, tv, toff, j, h2)) * inv_beta : 0.0;
         const double w = ok ? (au - row_dot<MAXC, SC>(R, tv, toff, j, g) - gj * vj) * inv_beta : 0.0;
@@ -1150,7 +1154,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 // step's record.  One banded SpMV from LDS (window halo as k_arn_d1); the basis row is loaded
 // only for the factor that tracks the Gram row.  Products and sums separately rounded like the
 // reference's broadcasts.  Columns written once (even j -> E, odd j -> the pair).
-template <int MAXC, int FMT>
+// (launched when some factor of the launch keeps a Gram row; otherwise k_lan_1w below)
+template <int MAXC, int FMT, bool G>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_lan_1s(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     constexpr int NG = (MAXC + 15) / 16;
@@ -1167,7 +1172,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     double* Uout = a.ubuf ? d.U : d.W;
     const double alpha = ld(d.sc, SC_ALPHA), ib = ld(d.sc, SC_INVBETA), betap = ld(d.sc, SC_BETAPREV);
     const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
-    const bool gram = d.track_gram != 0;
+    const bool gram = G && d.track_gram != 0;
     const int nch = 1 + (gram ? NG : 0);
     for (int k = t; k < nch * 64; k += TPB) acc[k] = 0.0;
     const int64_t S = (int64_t)slot * WS - 2 * hl;
@@ -1231,6 +1236,94 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             if (col < j) vi = 6 + col;
         }
         if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
+    }
+}
+
+// The same step when no factor of the launch keeps a Gram row (the deferred Gram): the
+// kernel moves 40-48 bytes per row and nothing else, so a 256-row block would be all
+// latency (load, barrier, SpMV, store, reduce for 11 KB).  Each thread takes LAN_RPT rows
+// of a window of LAN_RPT * 256 (loads of all its rows in flight together), the window owns
+// all but its hl + hu edge rows (one SpMV: v_j is computed pointwise on every row of the
+// window, u = A v_j - beta v_{j-1} is valid on the owned rows), and the block's dots are
+// summed per thread over its rows in row order, then reduce-scattered like k_lan_1s.
+// P1 = [ <u,v_j>, |u|^2, |v_j|^2, <v_j,b>, |wt|^2, <wt,v_j> ] at stride DFac::nwl.  (The
+// reduce stays a launch of its own: ending the step in the factor's last block to arrive
+// took ~1000 same-address agent atomics per factor and measured 10 us slower per step.)
+template <int FMT>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lan_1w(const DFac* __restrict__ F, KArgs a) {
+#pragma clang fp contract(off)
+    constexpr int RW = LAN_RPT * TPB;
+    __shared__ double xv[RW];
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const DFac& d = F[blockIdx.y];
+    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    if (slot >= d.nwl) return;
+    const int64_t TS = (int64_t)TPB * kcp(a.kmax);
+    double* acc = lds;   // [64]: 4 wave slots per value
+    const int j = a.j, t = threadIdx.x;
+    const int hl = d.hl, hu = d.hu;
+    const double* Uin = a.ubuf ? d.W : d.U;
+    double* Uout = a.ubuf ? d.U : d.W;
+    const double alpha = ld(d.sc, SC_ALPHA), ib = ld(d.sc, SC_INVBETA), betap = ld(d.sc, SC_BETAPREV);
+    const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
+    if (t < 64) acc[t] = 0.0;
+    const int64_t S = (int64_t)slot * (RW - hl - hu) - hl;
+    double up[LAN_RPT], vp[LAN_RPT], bv[LAN_RPT];
+#pragma unroll
+    for (int i = 0; i < LAN_RPT; ++i) {
+        const int64_t r = S + i * TPB + t;
+        const bool inb = r >= 0 && r < a.ld;
+        const bool ok = r >= 0 && r < a.n;
+        const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * 16) : 0x80000000u;
+        up[i] = inb ? ld(Uin, r) : 0.0;
+        // v_{j-1}: E after an even step, the odd half of its pair otherwise
+        vp[i] = j == 0 ? 0.0 : ((j & 1) ? (inb ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j - 1)));
+        bv[i] = ok ? ld(d.b, r) : 0.0;
+    }
+    double vj[LAN_RPT];
+#pragma unroll
+    for (int i = 0; i < LAN_RPT; ++i) {
+        const int64_t r = S + i * TPB + t;
+        const bool ok = r >= 0 && r < a.n;
+        const double w = sub_rn_(up[i], mul_rn(alpha, vp[i]));
+        vj[i] = ok ? mul_rn(ib, w) : 0.0;
+        xv[i * TPB + t] = vj[i];
+    }
+    __syncthreads();
+    double x[16] = {0.0};
+#pragma unroll
+    for (int i = 0; i < LAN_RPT; ++i) {
+        const int w = i * TPB + t;
+        const int64_t r = S + w;
+        const bool ok = r >= 0 && r < a.n;
+        const bool own = ok && w >= hl && w < RW - hu;
+        const double av = own ? spmv<FMT>(d.A, r, [&](int64_t cc) {
+            const int64_t q = cc - S;
+            return xv[q < 0 ? 0 : (q >= RW ? RW - 1 : (int)q)];
+        }) : 0.0;
+        const double u = own ? sub_rn_(av, mul_rn(betap, vp[i])) : 0.0;
+        if (own) {
+            if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj[i], vp[i]);
+            else st(d.E, r, vj[i]);
+            st(Uout, r, u);
+        }
+        const double vo = own ? vj[i] : 0.0;
+        // beta_j from dots of wt = u - alpha_{j-1} v_j (see k_lan_1s)
+        const double wt = own ? u - alpha * vo : 0.0;
+        x[0] += u * vo;
+        x[1] += u * u;
+        x[2] += vo * vo;
+        x[3] += vo * bv[i];
+        x[4] += wt * wt;
+        x[5] += wt * vo;
+    }
+    D1_ACC(0, x);   // (acc was zeroed before the barrier above)
+    __syncthreads();
+    if (t < 6) {
+        double sum = 0.0;
+#pragma unroll
+        for (int p = 0; p < D1_NP; ++p) sum += D1_PART(0, p, t);
+        st(d.P1, (int64_t)t * d.nwl + slot, sum);
     }
 }
 
@@ -1616,6 +1709,49 @@ __global__ __launch_bounds__(64) void k_reduce(const DFac* __restrict__ F, int w
 // four waves per value, each lane a strided subset in rounds of 16 independent loads, DPP
 // row sums, the 16 row totals summed in fixed order.
 __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent);
+// The one-sweep Lanczos step's end, in the block that has its reduced dots (every thread
+// alike): alpha_j = <u,v_j> (src/orthogonal_bases.jl:50), beta_j = ||u - alpha v_j|| (:56),
+// v_{j+1}'s scalars for the next step / the flush, and the step's record row (as POST_LAN:
+// H[j,j], H[j+1,j], btilde_j = <v_j,b>, the Gram row of v_j via gram(c)) written through,
+// with its host mirror, then the exchange / host signal.  al_est = alpha_{j-1}, the estimate
+// the sweep took wt = u - al_est v_j around.
+template <class G>
+__device__ void lan_step_record(const DFac& d, const KArgs& ax, int fidx, double al, double vv, double bt, double ww,
+                                double wv, double al_est, G gram) {
+#pragma clang fp contract(off)
+    const int t = threadIdx.x;
+    const int j = ax.j, kmax = ax.kmax;
+    // ||u - al v||^2 = ||wt + dl v||^2, dl = al_est - al: no cancellation of the size of
+    // alpha^2 (k_lan_1s)
+    const double dl = al_est - al;
+    const double bsq = add_rn(add_rn(ww, mul_rn(2.0 * dl, wv)), mul_rn(mul_rn(dl, dl), vv));
+    const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+    const double ib = beta == 0.0 ? 0.0 : 1.0 / beta;
+    if (t == 0) {
+        st(d.sc, SC_ALPHA, al);
+        st(d.sc, SC_INVBETA, ib);
+        st(d.sc, SC_BETA, beta);
+        st(d.sc, SC_BETAPREV, beta);
+        __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    double* rec = ax.rec + (int64_t)d.gidx * ax.m;
+    double* hr = ax.hdone ? ax.hrec + (int64_t)d.gidx * ax.m : nullptr;
+    const int g0 = rec_gram(kmax);
+    for (int i = t; i < ax.m; i += blockDim.x) {
+        double v = 0.0;
+        if (i == j) v = al;
+        else if (i == j + 1) v = beta;
+        else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? gram(i - g0) : vv) : 0.0;
+        else if (i == rec_beta(kmax)) v = beta;
+        else if (i == rec_bt(kmax)) v = bt;
+        else if (i == rec_col(kmax)) v = (double)j;
+        else if (i == rec_tracked(kmax)) v = d.track_gram ? 1.0 : 0.0;
+        __hip_atomic_store(rec + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (hr) __hip_atomic_store(hr + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    post_signal(ax, d, fidx, true, true);
+}
+
 // coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
 // RED_LAN: one-sweep Lanczos step (nv = 6 + j; 6 for factors without a Gram row; the last
 // block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
@@ -1629,7 +1765,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     if (coefJ == RED_LAN && !d.track_gram) nv = 6;
     if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
-    const int npart = np > 0 ? np : d.npd;
+    const int npart = np > 0 ? np : (np < 0 ? d.nwl : d.npd);   // (-1: k_lan_1w's windows)
     const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
     const int t = threadIdx.x;
     double s = 0.0;
@@ -1678,41 +1814,8 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     if (!last) return;
     auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     if (coefJ == RED_LAN) {
-        // alpha_j = <u,v_j> (src/orthogonal_bases.jl:50), beta_j = ||u - alpha v_j|| (:56) from
-        // the dots (every thread alike), v_{j+1}'s scalars for the next step / the flush, and
-        // the step's record row (as POST_LAN: H[j,j], H[j+1,j], btilde_j = <v_j,b>, the Gram
-        // row of v_j) written through, with its host mirror, then the exchange / host signal
-        const int j = ax.j, kmax = ax.kmax;
-        const double al = cld(0), vv = cld(2), bt = cld(3), ww = cld(4), wv = cld(5);
-        // ||u - al v||^2 = ||wt + dl v||^2, wt = u - al' v, dl = al' - al (al' = alpha_{j-1},
-        // the estimate the sweep used): no cancellation of the size of alpha^2 (k_lan_1s)
-        const double dl = al_est - al;
-        const double bsq = add_rn(add_rn(ww, mul_rn(2.0 * dl, wv)), mul_rn(mul_rn(dl, dl), vv));
-        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
-        const double ib = beta == 0.0 ? 0.0 : 1.0 / beta;
-        if (t == 0) {
-            st(d.sc, SC_ALPHA, al);
-            st(d.sc, SC_INVBETA, ib);
-            st(d.sc, SC_BETA, beta);
-            st(d.sc, SC_BETAPREV, beta);
-            __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        double* rec = ax.rec + (int64_t)d.gidx * ax.m;
-        double* hr = ax.hdone ? ax.hrec + (int64_t)d.gidx * ax.m : nullptr;
-        const int g0 = rec_gram(kmax);
-        for (int i = t; i < ax.m; i += 256) {
-            double v = 0.0;
-            if (i == j) v = al;
-            else if (i == j + 1) v = beta;
-            else if (i >= g0 && i <= g0 + j) v = d.track_gram ? (i - g0 < j ? cld(6 + i - g0) : vv) : 0.0;
-            else if (i == rec_beta(kmax)) v = beta;
-            else if (i == rec_bt(kmax)) v = bt;
-            else if (i == rec_col(kmax)) v = (double)j;
-            else if (i == rec_tracked(kmax)) v = d.track_gram ? 1.0 : 0.0;
-            __hip_atomic_store(rec + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (hr) __hip_atomic_store(hr + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        post_signal(ax, d, (int)blockIdx.y, true, true);
+        lan_step_record(d, ax, (int)blockIdx.y, cld(0), cld(2), cld(3), cld(4), cld(5), al_est,
+                        [&](int c) { return cld(6 + c); });
         return;
     }
     if (t >= 64) return;
@@ -2383,12 +2486,14 @@ void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 1, a.kmax, TK_A1_SCALAR ? 0 : 2);
-    with_fmt(a.fmt, [&](auto FM) {
+    auto go = [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
             hipLaunchKernelGGL((k_arn_a1_fused<decltype(M)::value, decltype(FM)::value>), dim3(a.npart, nf),
                                dim3(TPB), lds, s, F, a);
         });
-    });
+    };
+    if (a.mfs) go(IC<SPM_PRE>{});   // A U from k_spmv_mf
+    else with_fmt(a.fmt, go);
 }
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
@@ -2416,14 +2521,18 @@ void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t 
         hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
     });
 }
-void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, bool gram, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
-    const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
+    const dim3 grid((npd + 7) / 8 * 8, nf);
     with_band_fmt(a.fmt, [&](auto FM) {
+        if (!gram) {   // npd = the largest DFac::nwl of the launch
+            hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value>), grid, dim3(TPB), 64 * sizeof(double), s, F, a);
+            return;
+        }
+        const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
         with_maxc(a.j, [&](auto M) {
-            hipLaunchKernelGGL((k_lan_1s<decltype(M)::value, decltype(FM)::value>), dim3((npd + 7) / 8 * 8, nf),
-                               dim3(TPB), lds, s, F, a);
+            hipLaunchKernelGGL((k_lan_1s<decltype(M)::value, decltype(FM)::value, true>), grid, dim3(TPB), lds, s, F, a);
         });
     });
 }
@@ -2504,8 +2613,8 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     KArgs none;
     memset(&none, 0, sizeof(none));
-    if (npart <= 0 && !gate)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
+    if (npart <= 0 && !gate)   // (0: DFac::npd partials, -1: DFac::nwl)
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, coefJ, ax ? *ax : none);
     else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
         hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1, none);
     else
@@ -2548,7 +2657,7 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
         hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
 }
 #ifndef TK_GRAM_BLOCKS
-#define TK_GRAM_BLOCKS 1024   // k_gram blocks (4 per CU): a function of n only
+#define TK_GRAM_BLOCKS 512    // k_gram blocks (2 per CU; A/B in profiles/r03/gram_ab.txt): a function of n only
 #endif
 int gram_values(int k) { return k <= 32 ? 3 * 256 : 10 * 256; }
 int gram_blocks(int ntiles) { return ntiles < TK_GRAM_BLOCKS ? ntiles : TK_GRAM_BLOCKS; }

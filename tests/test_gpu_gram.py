@@ -7,7 +7,8 @@ device holds (entries are O(1) on the diagonal and O(eps) off it: absolute 1e-14
 1e-13 at n = 2^20, where each entry sums 2^20 products); k crosses the 32-column block edge
 and odd k exercises the masked last column of a pair.  The driver's orthogonality_data with
 a deferred Gram (TensorLanczos' default) must be rounding noise of the same size as with a
-Gram row per step, and the rest of the trajectory bitwise the same.
+Gram row per step, and the rest of the trajectory bitwise the same (TensorArnoldi) or equal to
+rounding (TensorLanczos, whose gram-free step is another kernel, k_lan_1w).
 """
 import numpy as np
 import pytest
@@ -78,8 +79,16 @@ def test_deferred_orthogonality_data(ctx, method, monkeypatch):
         conv.decomposition.close()
         out[mode] = conv
     r, q = out["rows"], out["deferred"]
-    assert np.array_equal(r.relative_residual_norm, q.relative_residual_norm)
-    assert np.array_equal(r.projected_residual_norm, q.projected_residual_norm)
+    if method == "TensorArnoldi":
+        assert np.array_equal(r.relative_residual_norm, q.relative_residual_norm)
+        assert np.array_equal(r.projected_residual_norm, q.projected_residual_norm)
+    else:
+        # without a Gram row the Lanczos step runs as k_lan_1w (wide windows): its dots are
+        # summed in another order than k_lan_1s', so alpha and beta differ in the last bits
+        for a_, b_ in ((r.relative_residual_norm, q.relative_residual_norm),
+                       (r.projected_residual_norm, q.projected_residual_norm)):
+            a_, b_ = np.asarray(a_[1:]), np.asarray(b_[1:])
+            assert np.abs(a_ - b_).max() <= 1e-9 * np.abs(a_).max(), np.abs(a_ - b_).max()
     o1, o2 = np.asarray(r.orthogonality_data[1:]), np.asarray(q.orthogonality_data[1:])
     assert np.all(np.isfinite(o2))
     if method == "TensorArnoldi":

@@ -252,20 +252,24 @@ def test_lanczos_one_sweep_beta_with_large_shift(ctx, shift):
     assert np.abs(beta / b_ref - 1).max() <= 1e-8, np.abs(beta / b_ref - 1).max()
 
 
+@pytest.mark.parametrize("gram", ["rows", "none"])
 @pytest.mark.parametrize("ttr", ["auto", "ttr"])
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20),
                                      ("Laplace", 700, 75)])
-def test_lanczos_matches_oracle(ctx, cls, n, K, ttr, monkeypatch):
-    """'auto': banded A_s take the one-sweep Lanczos (k_lan_1s; beyond step 63 the TTR
-    kernels), 'ttr': TKHIP_LANCZOS=ttr forces the three-pass TTR kernels."""
+def test_lanczos_matches_oracle(ctx, cls, n, K, ttr, gram, monkeypatch):
+    """'auto': banded A_s take the one-sweep Lanczos (beyond step 63 the TTR kernels), 'ttr':
+    TKHIP_LANCZOS=ttr forces the three-pass TTR kernels.  gram 'rows': every factor keeps a
+    Gram row (k_lan_1s); 'none': the deferred Gram of the driver, no factor keeps one
+    (k_lan_1w, multi-row windows) while kmax + 1 <= 64."""
     if ttr == "ttr":
         monkeypatch.setenv("TKHIP_LANCZOS", "ttr")
     else:
         monkeypatch.delenv("TKHIP_LANCZOS", raising=False)
+    monkeypatch.delenv("TKHIP_GRAM", raising=False)
     tk = _tk()
     csc = tk.assemble_matrix(n, cls)
     bs = _rhs(n, 2, 11, distinct=True)
-    recs, V = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K)
+    recs, V = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K, track_all=gram == "rows")
     for f, b in enumerate(bs):
         fo = O.Factor(csc, b, K)
         for j in range(1, K + 1):
@@ -279,6 +283,34 @@ def test_lanczos_matches_oracle(ctx, cls, n, K, ttr, monkeypatch):
         assert np.abs(beta - b_ref).max() <= 1e-12 * scale
         # TTR loses orthogonality; compare V only while the oracle's loss is small
         assert np.abs(V[f][:, :8] - fo.V[:, :8]).max() <= 1e-11
+
+
+@pytest.mark.parametrize("n,offs,K", [(2032, (-2, -1, 0, 1, 2), 30), (2033, (-2, -1, 0, 1, 2), 30),
+                                      (2040, (-2, -1, 0, 1, 2), 30), (1019, (-4, -1, 0, 1, 4), 25),
+                                      (3070, (-3, 0, 3), 20), (5, (-1, 0, 1), 3)])
+def test_lanczos_general_band_matches_oracle(ctx, n, offs, K, monkeypatch):
+    """One-sweep Lanczos without Gram rows (k_lan_1w) over symmetric non-Toeplitz bands of
+    half-bandwidth up to 4: its windows of LAN_RPT x 256 rows own all but hl + hu of them, n at
+    and around multiples of that stride (4 x 508 and 2 x 1020 for the 2- and 4-row windows at
+    hl = hu = 2), n < one window."""
+    monkeypatch.delenv("TKHIP_LANCZOS", raising=False)
+    monkeypatch.delenv("TKHIP_GRAM", raising=False)
+    tk = _tk()
+    B = _band(n, offs, 5)
+    csc = O.dense_to_csc(np.tril(B) + np.tril(B, -1).T)
+    bs = _rhs(n, 2, 6, distinct=True)
+    recs, V = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, K, track_all=False)
+    for f, b in enumerate(bs):
+        fo = O.Factor(csc, b, K)
+        for j in range(1, K + 1):
+            fo.lanczos_ttr(j)
+        alpha = np.array([recs[j + 1][f, j] for j in range(K)])
+        beta = np.array([recs[j + 1][f, j + 1] for j in range(K)])
+        scale = np.abs(fo.H[:K + 1, :K]).max()
+        assert np.abs(alpha - np.diag(fo.H[:K, :K])).max() <= 1e-12 * scale
+        assert np.abs(beta - np.diag(fo.H[1:K + 1, :K])).max() <= 1e-12 * scale
+        m = min(8, K + 1)
+        assert np.abs(V[f][:, :m] - fo.V[:, :m]).max() <= 1e-11
 
 
 def test_lanczos_reorth_matches_oracle(ctx):
@@ -381,16 +413,20 @@ def test_basis_mul_mfma(ctx):
     A.close()
 
 
-def test_lanczos_mid_run_flush(ctx):
+@pytest.mark.parametrize("gram", ["rows", "none"])
+def test_lanczos_mid_run_flush(ctx, gram, monkeypatch):
     """One-sweep Lanczos: reading the basis mid-run flushes the pending column (after an even
     step its predecessor is still in the column buffer); the run then continues and every
-    record and the final basis are bitwise those of the uninterrupted run."""
+    record and the final basis are bitwise those of the uninterrupted run (gram 'none': the
+    steps run as k_lan_1w)."""
+    monkeypatch.delenv("TKHIP_GRAM", raising=False)
     tk = _tk()
     csc = tk.assemble_matrix(1500, "Laplace")
     bs = _rhs(1500, 2, 23, distinct=True)
-    ra, Va = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20)
+    tr = gram == "rows"
+    ra, Va = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20, track_all=tr)
     for peek in (8, 11):
-        rb, Vb = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20, peek=peek)
+        rb, Vb = _run_device(ctx, tk._lib.TK_LANCZOS, csc, bs, 20, peek=peek, track_all=tr)
         for x, y in zip(ra[:-1], rb[:-1]):
             assert np.array_equal(x, y)
         for x, y in zip(Va, Vb):
@@ -398,9 +434,13 @@ def test_lanczos_mid_run_flush(ctx):
 
 
 @pytest.mark.parametrize("n,K", [(3000, 30), (1000, 70)])
-def test_lanczos_untracked_factors_identical(ctx, n, K):
+def test_lanczos_untracked_factors_identical(ctx, n, K, monkeypatch):
     """Factors without a Gram row take k_lan_d1's light path (no register row): their H
-    entries, b-tilde and basis are bitwise those of the same factors stepped with Gram rows."""
+    entries, b-tilde and basis are bitwise those of the same factors stepped with Gram rows.
+    (TKHIP_GRAM=rows: factor 0 keeps its row, so the one-sweep steps run as k_lan_1s for all
+    three; with no row at all they run as k_lan_1w, whose dots sum in another order --
+    test_lanczos_matches_oracle[none].)"""
+    monkeypatch.setenv("TKHIP_GRAM", "rows")
     tk = _tk()
     csc = tk.assemble_matrix(n, "Laplace")
     bs = _rhs(n, 3, 17, distinct=True)
