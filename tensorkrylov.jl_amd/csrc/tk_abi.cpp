@@ -653,6 +653,7 @@ struct tk_decomp {
     // been enqueued yet; the next step's k_arn_d1 runs it in a spare block (bk_args = the
     // step's KArgs), or bk_flush launches it on its own
     int bk_j = -1;
+    int bk_kind = 0;        // 0: k_arn_d1's bookkeeping (POST_ARN_D), 1: k_lan_1w's record signal
     KArgs bk_args;
     bool mfspmv = false;    // CGS2 factors sharing one A_s: one gather per nonzero for all (k_spmv_mf)
     // orthogonality_data of global factor 0 (src/tensor_krylov_method.jl:103) from one MFMA SYRK
@@ -1247,7 +1248,7 @@ static tk_status bk_flush(tk_decomp* dc) {
     const int j = dc->bk_j;
     const KArgs ax = dc->bk_args;
     dc->bk_j = -1;
-    RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, ax, POST_ARN_D, 0, 1, s), "post");
+    RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, ax, dc->bk_kind ? POST_SIGNAL : POST_ARN_D, 0, 1, s), "post");
     complete_step(dc, j, ax.seq);
     return TK_OK;
 }
@@ -1382,7 +1383,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         a.ubuf = j & 1;
         KArgs b = base_args(dc, -1, slot);
         b.j = -1;
-        if (dc->bk_j >= 0 && dc->bk_j == j - 1) b = dc->bk_args;
+        if (dc->bk_j >= 0 && dc->bk_j == j - 1 && dc->bk_kind == 0) b = dc->bk_args;
         else if (dc->bk_j >= 0) {
             tk_status st2 = bk_flush(dc);
             if (st2) return st2;
@@ -1392,6 +1393,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
         dc->bk_j = j;
         dc->bk_args = ax;
+        dc->bk_kind = 0;
         dc->pending = true;
     } else if (dc->method == TK_ARNOLDI) {
         const bool fused = dc->pending;
@@ -1414,9 +1416,31 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // one sweep: writes v_j (E or its pair) and u_j; the reduce's last block takes
         // alpha_j, beta_j and writes the step's record (no post launch)
         a.ubuf = j & 1;
-        // (no Gram row: k_lan_1w's wide windows, DFac::nwl partials -- np -1 to the reduce)
-        RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->any_gram ? dc->npd : dc->nwl, dc->any_gram, s), "lan_1s");
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, dc->any_gram ? 0 : -1, s, 0, RED_LAN, &ax), "reduce");
+        if (dc->any_gram) {
+            RUN(TCLS_PASS1, 2, launch_lan_1s(dc->df, nf, a, dc->npd, s), "lan_1s");
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, 0, s, 0, RED_LAN, &ax), "reduce");
+        } else {
+            // no Gram row: k_lan_1w's wide windows (DFac::nwl partials -- np -1 to the reduce).
+            // The record's host mirror and signal are deferred to leading blocks of the next
+            // step's launch (as k_arn_d1's bookkeeping): the reduce that ends the step -- on
+            // the path to the next step -- then waits for no host-memory stores
+            KArgs b = base_args(dc, -1, slot);
+            b.j = -1;
+            if (dc->bk_j >= 0 && dc->bk_j == j - 1 && dc->bk_kind == 1) b = dc->bk_args;
+            else if (dc->bk_j >= 0) {
+                tk_status st2 = bk_flush(dc);
+                if (st2) return st2;
+            }
+            RUN(TCLS_PASS1, 2, launch_lan_1w(dc->df, nf, a, b, dc->nwl, s), "lan_1w");
+            KArgs an = ax;
+            an.xflag = nullptr;
+            an.hdone = nullptr;
+            an.hrec = nullptr;
+            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, -1, s, 0, RED_LAN, &an), "reduce");
+            dc->bk_j = j;
+            dc->bk_args = ax;
+            dc->bk_kind = 1;
+        }
         dc->pending = true;
     } else if (dc->method == TK_LANCZOS) {
         const bool fused = dc->pending;

@@ -140,7 +140,10 @@ void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
-void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, bool gram, hipStream_t s);
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
+// the gram-free one-sweep Lanczos step (k_lan_1w; npd = the largest DFac::nwl); b.j >= 0: the
+// previous step's record mirror + signal ride in 8 leading blocks
+void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
 // rows per thread of k_lan_1w (its windows are LAN_RPT * 256 rows; 2: 67 us per C2 step
 // against 71 at 4 and 77 at 8, profiles/r03/lan_rpt_ab.txt)
 #ifndef TK_LAN_RPT

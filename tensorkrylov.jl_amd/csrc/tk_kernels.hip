@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 // only for the factor that tracks the Gram row.  Products and sums separately rounded like the
 // reference's broadcasts.  Columns written once (even j -> E, odd j -> the pair).
 // (launched when some factor of the launch keeps a Gram row; otherwise k_lan_1w below)
-template <int MAXC, int FMT, bool G>
+template <int MAXC, int FMT>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_lan_1s(const DFac* __restrict__ F, KArgs a) {
 #pragma clang fp contract(off)
     constexpr int NG = (MAXC + 15) / 16;
@@ -1172,7 +1172,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     double* Uout = a.ubuf ? d.U : d.W;
     const double alpha = ld(d.sc, SC_ALPHA), ib = ld(d.sc, SC_INVBETA), betap = ld(d.sc, SC_BETAPREV);
     const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
-    const bool gram = G && d.track_gram != 0;
+    const bool gram = d.track_gram != 0;
     const int nch = 1 + (gram ? NG : 0);
     for (int k = t; k < nch * 64; k += TPB) acc[k] = 0.0;
     const int64_t S = (int64_t)slot * WS - 2 * hl;
@@ -1250,13 +1250,23 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 // reduce stays a launch of its own: ending the step in the factor's last block to arrive
 // took ~1000 same-address agent atomics per factor and measured 10 us slower per step.)
 template <int FMT>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lan_1w(const DFac* __restrict__ F, KArgs a) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lan_1w(const DFac* __restrict__ F, KArgs a,
+                                                                                          KArgs b) {
 #pragma clang fp contract(off)
     constexpr int RW = LAN_RPT * TPB;
     __shared__ double xv[RW];
     extern __shared__ __attribute__((aligned(16))) double lds[];
+    // b.j >= 0: 8 leading blocks (one per XCD; dispatched first, done while the windows
+    // stream) mirror the previous step's record rows to the host and signal them
+    const int x0 = b.j >= 0 ? 8 : 0;
+    if ((int)blockIdx.x < x0) {
+        if (blockIdx.y == 0)
+            for (int f = blockIdx.x; f < (int)gridDim.y; f += 8) post_signal(b, F[f], f, false);
+        return;
+    }
     const DFac& d = F[blockIdx.y];
-    const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
+    const int bx = (int)blockIdx.x - x0;   // (x0 is a multiple of 8: the XCD of bx is kept)
+    const int slot = (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
     if (slot >= d.nwl) return;
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     double* acc = lds;   // [64]: 4 wave slots per value
@@ -2521,19 +2531,22 @@ void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t 
         hipLaunchKernelGGL((k_init_bd<decltype(FM)::value>), dim3(npd, nf), dim3(TPB), lds_bytes(3, a.kmax, 0), s, F, a);
     });
 }
-void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, bool gram, hipStream_t s) {
+void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
-    const dim3 grid((npd + 7) / 8 * 8, nf);
+    const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
     with_band_fmt(a.fmt, [&](auto FM) {
-        if (!gram) {   // npd = the largest DFac::nwl of the launch
-            hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value>), grid, dim3(TPB), 64 * sizeof(double), s, F, a);
-            return;
-        }
-        const size_t lds = (size_t)(1 + (M + 15) / 16) * 64 * sizeof(double);
         with_maxc(a.j, [&](auto M) {
-            hipLaunchKernelGGL((k_lan_1s<decltype(M)::value, decltype(FM)::value, true>), grid, dim3(TPB), lds, s, F, a);
+            hipLaunchKernelGGL((k_lan_1s<decltype(M)::value, decltype(FM)::value>), dim3((npd + 7) / 8 * 8, nf),
+                               dim3(TPB), lds, s, F, a);
         });
+    });
+}
+void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
+    const dim3 grid((npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0), nf);
+    with_band_fmt(a.fmt, [&](auto FM) {
+        hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
     });
 }
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
