@@ -1405,6 +1405,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             }
             RUN(TCLS_PASS1, 2, launch_arn_a1_fused(dc->df, nf, a, s), "arn_a1_fused");
         } else {
+            if (dc->mfspmv && j == 0) {   // (k_init_b left U = v_0)
+                RUN(TCLS_PASS1, 2, launch_spmv_mf(dc->df, nf, a, s), "spmv_mf");
+                a.mfs = 1;
+            }
             RUN(TCLS_PASS1, 2, launch_arn_a1_plain(dc->df, nf, a, s), "arn_a1_plain");
         }
         RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, j + 1, dc->npart, s), "reduce");
@@ -1436,7 +1440,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             an.xflag = nullptr;
             an.hdone = nullptr;
             an.hrec = nullptr;
-            RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 6 + j, -1, s, 0, RED_LAN, &an), "reduce");
+            RUN(TCLS_RED, 2, launch_red_lan(dc->df, nf, an, s), "red_lan");
             dc->bk_j = j;
             dc->bk_args = ax;
             dc->bk_kind = 1;

@@ -144,6 +144,8 @@ void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s
 // the gram-free one-sweep Lanczos step (k_lan_1w; npd = the largest DFac::nwl); b.j >= 0: the
 // previous step's record mirror + signal ride in 8 leading blocks
 void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s);
+// ... and its reduce: one 1024-thread block per factor ends the step (alpha, beta, record)
+void launch_red_lan(const DFac* F, int nf, const KArgs& ax, hipStream_t s);
 // rows per thread of k_lan_1w (its windows are LAN_RPT * 256 rows; 2: 67 us per C2 step
 // against 71 at 4 and 77 at 8, profiles/r03/lan_rpt_ab.txt)
 #ifndef TK_LAN_RPT

@@ -553,6 +553,7 @@ __global__ __launch_bounds__(TPB) void k_init_b(const DFac* __restrict__ F, KArg
         const double bv = ld(d.b, r);
         const double v0 = inv * bv;
         st_pair(d.V, (int64_t)tile * TS, 0, threadIdx.x, v0, 0.0);   // column 1 not yet written
+        if (d.Uint) st(d.U, r, v0);   // (shared A_s: step 0's A v0 from k_spmv_mf, which reads U)
         const double e[2] = {v0 * bv, v0 * v0};
         reduce_scalars<2>(e, tr, acc, 0, first);
     }
@@ -673,7 +674,9 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(A1_L4(FMT), A1_L3(FMT)) void k_arn_a1
         Row<MAXC> R;
         R.load(tv, toff, nc);
         const double* Vg = d.V;
-        const double w = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + vofs(j, (int)(c & 255))); }) : 0.0;
+        double w = 0.0;
+        if constexpr (FMT == SPM_PRE) w = ok ? ld(d.AU, r) : 0.0;   // (A v_j from k_spmv_mf)
+        else w = ok ? spmv<FMT>(d.A, r, [=](int64_t c) { return ld(Vg, (c >> 8) * TS + vofs(j, (int)(c & 255))); }) : 0.0;
         st(d.W, r, w);
         reduce_row<MAXC>(R, tv, toff, nc, w, tr, acc, 0, first);
     }
@@ -1762,6 +1765,49 @@ __device__ void lan_step_record(const DFac& d, const KArgs& ax, int fidx, double
     post_signal(ax, d, fidx, true, true);
 }
 
+// The gram-free one-sweep Lanczos step's reduce (k_lan_1w's 6 values over DFac::nwl
+// partials) in ONE block of 1024 threads per factor: every partial of the step loaded in one
+// round (<= 3 per value per thread up to nwl = 3072), summed per thread in order, DPP row sums,
+// the 64 row totals in fixed order -- then alpha, beta and the record in the same block: no
+// arrival counting between blocks (k_reduce256's six blocks and their hand-off measured
+// ~6 us per step, most of it the chain load -> coherent store -> atomic -> load).
+__global__ __launch_bounds__(1024) void k_red_lan(const DFac* __restrict__ F, KArgs ax) {
+    __shared__ double rs[6][64];
+    __shared__ double red[6];
+    const DFac& d = F[blockIdx.x];
+    const int t = threadIdx.x, np = d.nwl;
+    // (read before the barrier below: thread 0 overwrites it in lan_step_record)
+    const double al_est = ld(d.sc, SC_ALPHA);
+    double sv[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int p0 = 0; p0 < np; p0 += 3 * 1024) {
+        double q[3][6];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) {
+                const int p = p0 + k * 1024 + t;
+                q[k][c] = p < np ? ld(d.P1, (int64_t)c * np + p) : 0.0;
+            }
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+            for (int c = 0; c < 6; ++c) sv[c] += q[k][c];
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const double r = row16_sum(sv[c]);
+        if ((t & 15) == 0) rs[c][t >> 4] = r;
+    }
+    __syncthreads();
+    if (t < 6) {
+        double r = 0.0;
+        for (int q = 0; q < 64; ++q) r += rs[t][q];
+        red[t] = r;
+    }
+    __syncthreads();
+    lan_step_record(d, ax, (int)blockIdx.x, red[0], red[2], red[3], red[4], red[5], al_est, [](int) { return 0.0; });
+}
+
 // coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
 // RED_LAN: one-sweep Lanczos step (nv = 6 + j; 6 for factors without a Gram row; the last
 // block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
@@ -1775,7 +1821,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     if (coefJ == RED_LAN && !d.track_gram) nv = 6;
     if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
-    const int npart = np > 0 ? np : (np < 0 ? d.nwl : d.npd);   // (-1: k_lan_1w's windows)
+    const int npart = np > 0 ? np : d.npd;
     const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
     const int t = threadIdx.x;
     double s = 0.0;
@@ -2467,12 +2513,14 @@ void launch_init_b(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
 void launch_arn_a1_plain(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const size_t lds = lds_bytes(a.j + 1, a.kmax, 0);
-    with_fmt(a.fmt, [&](auto FM) {
+    auto go = [&](auto FM) {
         with_maxc(a.j + 1, [&](auto M) {
             hipLaunchKernelGGL((k_arn_a1_plain<decltype(M)::value, decltype(FM)::value>), dim3(a.npart, nf),
                                dim3(TPB), lds, s, F, a);
         });
-    });
+    };
+    if (a.mfs) go(IC<SPM_PRE>{});   // A v_j from k_spmv_mf
+    else with_fmt(a.fmt, go);
 }
 void launch_spmv_mf(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
@@ -2541,6 +2589,10 @@ void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s
                                dim3(TPB), lds, s, F, a);
         });
     });
+}
+void launch_red_lan(const DFac* F, int nf, const KArgs& ax, hipStream_t s) {
+    if (nf <= 0) return;
+    hipLaunchKernelGGL(k_red_lan, dim3(nf), dim3(1024), 0, s, F, ax);
 }
 void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
@@ -2626,8 +2678,8 @@ void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStrea
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     KArgs none;
     memset(&none, 0, sizeof(none));
-    if (npart <= 0 && !gate)   // (0: DFac::npd partials, -1: DFac::nwl)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, coefJ, ax ? *ax : none);
+    if (npart <= 0 && !gate)
+        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
     else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
         hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1, none);
     else
