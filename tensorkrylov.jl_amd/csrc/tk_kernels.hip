@@ -287,6 +287,31 @@ __device__ __forceinline__ void st_pair(double* V, int64_t tile_base, int c, int
     GP(d2_t, V + tile_base + vofs(c & ~1, t))[0] = x;
 }
 
+// The one-sweep Arnoldi step's outputs -- u, v_j, the window partials -- are read by the next
+// launches, not by this one: stored write-through (sc1), they leave no dirty lines in the XCD
+// L2s for the kernel boundary's writeback to drain (a boundary costs ~1.7 us + dirty bytes /
+// 6 TB/s, /opt/skills/guides/MI355X_MICROARCH.md "boundary"; plain stores keep the line dirty
+// in L2, sc1 stores drop it, "stores of each flavour").  Measured (profiles/r03/wt_ab.txt):
+// k_arn_d1 at one factor per GPU 2 us faster per step, neutral at 8 factors; k_lan_1w's
+// 8-byte stores 10 % slower write-through, so it keeps plain stores.  TK_WT=0: plain.
+#ifndef TK_WT
+#define TK_WT 1
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_wt(double* p, int64_t i, double v) {
+#if TK_WT
+    __hip_atomic_store(GP(double, p) + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    GP(double, p)[i] = v;
+#endif
+}
+// column pair (c & ~1, c | 1) of the row at byte offset toff of the basis resource
+__device__ __forceinline__ void st_pair_wt(rsrc_t basis, uint32_t toff, int c, double v, double other) {
+    const d2_t x = (c & 1) ? (d2_t){other, v} : (d2_t){v, other};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, x), basis, toff + (uint32_t)(c >> 1) * (TPB * 16), 0,
+                                           TK_WT ? 16 : 0);
+}
+
 // sum_c V[r,c] * h[c] for c < nc.  SCALAR: h is a global coefficient array read with
 // wave-uniform addresses through the constant address space (scalar loads, many in
 // flight); otherwise h is an LDS copy (broadcast reads).  Entries past nc are finite
@@ -1023,9 +1048,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         D1_PHASE(2);
         const bool own = ok && t >= 2 * hl && t < TPB - 2 * hu;
         if (own) {
-            if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj, R.last);   // (v_{j-1}, v_j)
-            else st(d.E, r, vj);
-            st(Uout, r, u);
+            if (j & 1) st_pair_wt(tv, toff, j, vj, R.last);   // (v_{j-1}, v_j)
+            else st_wt(d.E, r, vj);
+            st_wt(Uout, r, u);
         }
         const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
         // update_rhs!'s <v_j, b> as norm(b) * <v_j, v_0> (b = norm(b) v_0, src/decompositions.jl:
@@ -1132,7 +1157,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
             if (col < j) vi = 2 * j + 6 + col;
         }
-        if (vi >= 0) st(d.P1, (int64_t)vi * d.npd + slot, sum);
+        if (vi >= 0) st_wt(d.P1, (int64_t)vi * d.npd + slot, sum);
     }
 #if TK_D1_TRACE
     __syncthreads();
