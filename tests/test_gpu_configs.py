@@ -1,9 +1,9 @@
-"""GPU parity at the BASELINE.json workload sizes that are not n = 2^20 (C2 is covered in
-test_gpu_properties.py): every kernel variant the bench runs on C1, C3 and C4 is checked
+"""GPU parity at the BASELINE.json workload sizes: every kernel variant the bench runs on C1-C4 is checked
 here at exactly the bench's n, d and K, through the C ABI, against the C restatement of
 the reference (oracle/tk_ref.c: CSC-scatter SpMV + MGS2 / TTR in the reference's order,
 src/orthogonal_bases.jl:15-67), on the same seeded inputs.
 
+  * C2: d = 8, n = 2^20 Laplace, K = 50, all 8 factors (the headline bench workload).
   * C1: d = 4, n = 2^18 Laplace, K = 50, all 4 factors (one-sweep Arnoldi; its window
     count and reduce-partial count differ from C2's).
   * C3: d = 5, n = 2^19 random sparse SPD (~15 nnz/row, SELL-256 storage, two-sweep
@@ -102,6 +102,13 @@ def _check_arnoldi(ctx, cls, n, d, K, check, expect_sweeps, expect_format=None, 
     dev.close()
     A.close()
     return worst
+
+
+def test_c2_laplace_2p20_all_8_factors(ctx):
+    """C2 (BASELINE.json configs[2], the bench's headline workload): d = 8, n_s = 2^20 Laplace,
+    K = 50, all eight factors stepped in one decomposition exactly as bench.py does and every
+    one of them checked against the C oracle (C2 was checked with 2 factors)."""
+    _check_arnoldi(ctx, "Laplace", 1 << 20, 8, 50, check=range(8), expect_sweeps=1)
 
 
 def test_c1_laplace_2p18_all_factors(ctx):
