@@ -252,6 +252,37 @@ def test_lanczos_one_sweep_beta_with_large_shift(ctx, shift):
     assert np.abs(beta / b_ref - 1).max() <= 1e-8, np.abs(beta / b_ref - 1).max()
 
 
+@pytest.mark.parametrize("shift", [1e4, 1e6])
+def test_arnoldi_one_sweep_with_large_shift(ctx, shift):
+    """ADVICE r2 (the Arnoldi counterpart of the Lanczos case above): the one-sweep Arnoldi takes
+    beta = sqrt(|u|^2 - |c|^2) from dots, but of u already projected once (first CGS pass, the
+    delayed reorthogonalization's c is O(loss of orthogonality) small), so no alpha-sized
+    cancellation enters it; the diagonal cancels A v_j's sigma v_j against gamma v_j exactly as
+    the reference's MGS does (relative error eps sigma / beta on both sides).
+    tridiag(-1, 2 + shift, -1), the one-sweep storage (Toeplitz band)."""
+    tk = _tk()
+    n, K = 5000, 20
+    colptr, rowval, nz = tk.assemble_matrix(n, "Laplace")
+    nz = np.where(nz > 0, 2.0 + shift, -1.0)
+    csc = (colptr, rowval, nz)
+    bs = _rhs(n, 1, 13, distinct=True)
+    recs, V = _run_device(ctx, tk._lib.TK_ARNOLDI, csc, bs, K, sweeps=1)
+    fo = _arnoldi_oracle(csc, bs[0], K)
+    Hd = np.zeros((K + 1, K))
+    for j in range(K):
+        Hd[:j + 2, j] = recs[j + 1][0, :j + 2]
+    Hr = fo.H[:K + 1, :K]
+    beta = np.diag(Hr, -1)
+    ratio = shift / beta.min()
+    # diagonal (~shift): to eps times the problem's conditioning; subdiagonal (~1): each to
+    # its own magnitude; the rest (0 in exact arithmetic) at eps * shift
+    assert np.abs(np.diag(Hd) / np.diag(Hr) - 1).max() <= max(1e-13, 1e-15 * ratio)
+    assert np.abs(np.diag(Hd, -1) / beta - 1).max() <= max(1e-12, 1e-15 * ratio), np.abs(np.diag(Hd, -1) / beta - 1).max()
+    off = np.triu(Hd - Hr, 1)
+    assert np.abs(off).max() <= 1e-14 * shift * 10
+    assert np.abs(V[0] - fo.V[:, :K + 1]).max() <= max(1e-12, 1e-15 * ratio)
+
+
 @pytest.mark.parametrize("gram", ["rows", "none"])
 @pytest.mark.parametrize("ttr", ["auto", "ttr"])
 @pytest.mark.parametrize("cls,n,K", [("Laplace", 200, 30), ("Laplace", 1000, 60), ("ConvDiff", 500, 20),
