@@ -1784,21 +1784,7 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         HIPCHK(hipStreamSynchronize(s));
         v = vbuf.data();
     }
-    // k_gram's layout: group pair i (ga <= gb), register r, lane l -> G[col(ga, m), col(gb, n)]
-    // with m = (l>>4) + 4r, n = l&15, col(g, x) = 32 (g>>1) + 2x + (g&1)
-    const int ngr = k <= 32 ? 2 : 4;
-    auto col = [](int g, int x) { return 32 * (g >> 1) + 2 * x + (g & 1); };
-    int i = 0;
-    for (int ga = 0; ga < ngr; ++ga)
-        for (int gb = ga; gb < ngr; ++gb, ++i)
-            for (int r = 0; r < 4; ++r)
-                for (int l = 0; l < 64; ++l) {
-                    const int p = col(ga, (l >> 4) + 4 * r), q = col(gb, l & 15);
-                    if (p >= k || q >= k) continue;
-                    const double x = v[(size_t)(i * 4 + r) * 64 + l];
-                    G[(size_t)q * k + p] = x;
-                    G[(size_t)p * k + q] = x;
-                }
+    gram_unpack(k, v, G);
     return TK_OK;
     TK_API_END
 }

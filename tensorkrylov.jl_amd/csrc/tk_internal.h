@@ -193,6 +193,8 @@ inline size_t gram_result_offset(int ntiles, int k) {
     return (size_t)(gram_blocks(ntiles) + 64) * gram_values(k);
 }
 void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s);
+// the gram_values(k) results -> G (k x k, both triangles)
+void gram_unpack(int k, const double* v, double* G);
 
 // record field offsets (see include/tk.h)
 __host__ __device__ inline int rec_len(int kmax) { return 2 * kmax + 10; }

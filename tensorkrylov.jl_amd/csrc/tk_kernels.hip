@@ -2392,31 +2392,53 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
 // SYRK on v_mfma_f64_16x16x4f64 (k <= 64): the MFMA's k-dimension runs over 4 basis rows, so
 // the sum over n -- what per-step Gram rows spend DPP reduce-scatters on -- happens in the
 // matrix core, and the basis is read once for all k columns instead of once per step.
-// One dwordx4 per lane fetches V[row, 2p .. 2p+1] of the paired-column tile: lane l (row slot
-// l>>4 of a 4-row quad, pair p = 16b + (l&15)) feeds column group 2b (even columns of 32-column
-// block b) and 2b+1 (odd columns).  For group pairs ga <= gb:
+// Column groups of 16 (lane l: row slot l>>4 of a 4-row quad, column (l&15) of the group):
+//   group 0 / 1 = even / odd columns of 0..31 (one dwordx4 per lane: pair l&15),
+//   group 2+g   = columns 32+16g .. 32+16g+15 (one dwordx2 per lane), g < NC16,
+// and TAIL (<= 4) columns K0 = 32+16 NC16 .. k-1 that would fill a group of 16 by a quarter
+// or less are formed on the VALU instead (all lanes load the tail pairs of their row: each
+// lane multiplies the tail entries by its own group entries, and lane l&15 < TAIL by tail
+// column l&15) -- at k = 50, 6 MFMA tiles per quad instead of 10 (the padded 16-column
+// group had 2 live columns), which left the launch MFMA-bound at 58 % pipe use.
 //   A = V[4 rows, group ga]'   lane l: column (l&15) of ga, row slot l>>4
 //   B = V[4 rows, group gb]    lane l: row slot l>>4, column (l&15) of gb
-//   D[m][n] = G[col(ga, m)][col(gb, n)],  lane l, reg i: m = (l>>4) + 4i, n = l&15,
-// col(g, i) = 32 (g>>1) + 2i + (g&1).  Blocks walk tiles (tile += gridDim.x, the grid a
-// function of n only); the 4 waves' accumulators are summed in fixed order through LDS and
-// each block writes its partial Pg[block][value]; k_gram_reduce sums partials in block order.
+//   D[m][n] = G[col(ga, m)][col(gb, n)],  lane l, reg i: m = (l>>4) + 4i, n = l&15.
+// Blocks walk tiles (tile += gridDim.x, the grid a function of n only); the 4 waves'
+// accumulators (and the tail's 4 row slots) are summed in fixed order through LDS and each
+// block writes its partial Pg[block][value]; k_gram_reduce sums partials in block order.
+// Values: NT tiles of 256 (group pairs ga <= gb), then with a tail 256 more: [a*64 + c] =
+// G[K0 + a][c], c < K0 + TAIL (gram_unpack decodes both).
 #ifndef TK_GRAM_GQ
 #define TK_GRAM_GQ 8   // row quads whose loads are in flight before their MFMAs
 #endif
-template <int NBLK>
+template <int NC16, int TAIL>
 __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs a, int f, int k,
                                               double* __restrict__ Pg) {
-    constexpr int NGR = 2 * NBLK;
+    constexpr int NGR = 2 + NC16;
     constexpr int NT = NGR * (NGR + 1) / 2;
-    __shared__ double red[NT * 4 * 64];
+    constexpr int K0 = 32 + 16 * NC16;
+    constexpr int NS = NGR + 1;              // tail products per lane and tail column
+    constexpr int NTP = (TAIL + 1) / 2;      // tail pairs
+    constexpr int TA = TAIL > 0 ? TAIL : 1;
+    __shared__ double red[NT * 4 * 64 + TAIL * NS * 256];
     const DFac& d = F[f];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, kr = lane >> 4, ci = lane & 15;
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     f64x4 acc[NT];
 #pragma unroll
     for (int i = 0; i < NT; ++i) acc[i] = (f64x4){0.0, 0.0, 0.0, 0.0};
-    const bool ev0 = 2 * ci < k, od0 = 2 * ci + 1 < k, ev1 = 2 * (16 + ci) < k, od1 = 2 * (16 + ci) + 1 < k;
+    double tac[TA][NS];
+#pragma unroll
+    for (int x = 0; x < TA; ++x)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) tac[x][s] = 0.0;
+    const bool ev = 2 * ci < k, od = 2 * ci + 1 < k;
+    bool cm[NC16 > 0 ? NC16 : 1];
+#pragma unroll
+    for (int g = 0; g < NC16; ++g) cm[g] = 32 + 16 * g + ci < k;
+    const int gq = w * 64 + kr;   // row of quad 0 of this lane
+    // (loads of the next batch issued before this batch's MFMAs -- ping-pong buffers -- measured
+    // 8-20 % slower: the register budget drops the launch to fewer waves)
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(k));
         // GQ row quads' loads in flight before their MFMAs (pairs past k read 0; the odd
@@ -2424,27 +2446,45 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
         constexpr int GQ = TK_GRAM_GQ;
 #pragma unroll 1
         for (int q0 = 0; q0 < 16; q0 += GQ) {
-            d2_t x[GQ][NBLK];
+            d2_t x[GQ];
+            double y[GQ][NC16 > 0 ? NC16 : 1];
+            d2_t tl[GQ][NTP > 0 ? NTP : 1];
 #pragma unroll
-            for (int q = 0; q < GQ; ++q)
+            for (int q = 0; q < GQ; ++q) {
+                const uint32_t row = (uint32_t)(gq + (q0 + q) * 4);
+                x[q] = bld2(tv, ((uint32_t)ci * TPB + row) * 16u);
 #pragma unroll
-                for (int b = 0; b < NBLK; ++b)
-                    x[q][b] = bld2(tv, ((uint32_t)(16 * b + ci) * TPB + w * 64 + (q0 + q) * 4 + kr) * 16u);
+                for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, cofs(32 + 16 * g + ci) + row * 16u);
+#pragma unroll
+                for (int p = 0; p < NTP; ++p) tl[q][p] = bld2(tv, ((uint32_t)(K0 / 2 + p) * TPB + row) * 16u);
+            }
 #pragma unroll
             for (int q = 0; q < GQ; ++q) {
                 double v[NGR];
-                v[0] = ev0 ? x[q][0].x : 0.0;
-                v[1] = od0 ? x[q][0].y : 0.0;
-                if (NBLK > 1) {
-                    v[NBLK > 1 ? 2 : 0] = ev1 ? x[q][NBLK - 1].x : 0.0;
-                    v[NBLK > 1 ? 3 : 1] = od1 ? x[q][NBLK - 1].y : 0.0;
-                }
+                v[0] = ev ? x[q].x : 0.0;
+                v[1] = od ? x[q].y : 0.0;
+#pragma unroll
+                for (int g = 0; g < NC16; ++g) v[2 + g] = cm[g] ? y[q][g] : 0.0;
                 int i = 0;
 #pragma unroll
                 for (int ga = 0; ga < NGR; ++ga)
 #pragma unroll
                     for (int gb = ga; gb < NGR; ++gb, ++i)
                         acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i], 0, 0, 0);
+                if (TAIL > 0) {
+                    double tt[TA];
+#pragma unroll
+                    for (int x2 = 0; x2 < TA; ++x2) tt[x2] = (x2 & 1) ? tl[q][x2 >> 1].y : tl[q][x2 >> 1].x;
+                    double own = 0.0;   // tail column ci of this row (lanes ci < TAIL)
+#pragma unroll
+                    for (int x2 = 0; x2 < TA; ++x2) own = ci == x2 ? tt[x2] : own;
+#pragma unroll
+                    for (int x2 = 0; x2 < TA; ++x2) {
+#pragma unroll
+                        for (int s = 0; s < NGR; ++s) tac[x2][s] = fma(tt[x2], v[s], tac[x2][s]);
+                        tac[x2][NGR] = fma(tt[x2], own, tac[x2][NGR]);
+                    }
+                }
             }
         }
     }
@@ -2461,7 +2501,31 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
         }
         __syncthreads();
     }
-    for (int e = threadIdx.x; e < NT * 256; e += 256) GP(double, Pg)[(int64_t)blockIdx.x * NT * 256 + e] = red[e];
+    double* trd = red + NT * 256;
+    if (TAIL > 0) {
+#pragma unroll
+        for (int x2 = 0; x2 < TA; ++x2)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) trd[((x2 * NS + s) * 4 + w) * 64 + lane] = tac[x2][s];
+        __syncthreads();
+    }
+    auto out = GP(double, Pg) + (int64_t)blockIdx.x * (NT * 256 + (TAIL > 0 ? 256 : 0));
+    for (int e = threadIdx.x; e < NT * 256; e += 256) out[e] = red[e];
+    if (TAIL > 0) {
+        // entry (x2, c): slot s and lane column of the products that formed it, summed over
+        // waves and row slots in fixed order
+        const int x2 = threadIdx.x >> 6, c = threadIdx.x & 63;
+        double sum = 0.0;
+        if (x2 < TAIL && c < K0 + TAIL) {
+            int s, cc;
+            if (c < 32) { s = c & 1; cc = c >> 1; }
+            else if (c < K0) { s = 2 + ((c - 32) >> 4); cc = (c - 32) & 15; }
+            else { s = NGR; cc = c - K0; }
+            for (int ww = 0; ww < 4; ++ww)
+                for (int r = 0; r < 4; ++r) sum += trd[((x2 * NS + s) * 4 + ww) * 64 + r * 16 + cc];
+        }
+        out[NT * 256 + threadIdx.x] = sum;
+    }
 }
 
 // out[s][v] = sum over partials b in [s*seg, min(nb, (s+1)*seg)) of P[b][v], in b order
@@ -2749,18 +2813,62 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
 #ifndef TK_GRAM_BLOCKS
 #define TK_GRAM_BLOCKS 512    // k_gram blocks (2 per CU; A/B in profiles/r03/gram_ab.txt): a function of n only
 #endif
-int gram_values(int k) { return k <= 32 ? 3 * 256 : 10 * 256; }
+// column groups of k_gram for k columns: NC16 runs of 16 beyond column 32, TAIL (<= 4) on the VALU
+static void gram_config(int k, int& nc16, int& tail) {
+    nc16 = 0;
+    tail = 0;
+    if (k <= 32) return;
+    nc16 = (k - 32) / 16;
+    tail = (k - 32) % 16;
+    if (tail > 4) {   // a group of 16 with more than 4 live columns: padded MFMA group
+        ++nc16;
+        tail = 0;
+    }
+}
+int gram_values(int k) {
+    int nc16, tail;
+    gram_config(k, nc16, tail);
+    const int ngr = 2 + nc16;
+    return ngr * (ngr + 1) / 2 * 256 + (tail ? 256 : 0);
+}
 int gram_blocks(int ntiles) { return ntiles < TK_GRAM_BLOCKS ? ntiles : TK_GRAM_BLOCKS; }
 size_t gram_scratch_doubles(int ntiles) { return (size_t)(gram_blocks(ntiles) + 64 + 1) * 10 * 256; }
+void gram_unpack(int k, const double* v, double* G) {
+    int nc16, tail;
+    gram_config(k, nc16, tail);
+    const int ngr = 2 + nc16, k0 = 32 + 16 * nc16;
+    auto col = [](int g, int x) { return g < 2 ? 2 * x + g : 32 + 16 * (g - 2) + x; };
+    int i = 0;
+    for (int ga = 0; ga < ngr; ++ga)
+        for (int gb = ga; gb < ngr; ++gb, ++i)
+            for (int r = 0; r < 4; ++r)
+                for (int l = 0; l < 64; ++l) {
+                    const int p = col(ga, (l >> 4) + 4 * r), q = col(gb, l & 15);
+                    if (p >= k || q >= k) continue;
+                    const double x = v[(size_t)(i * 4 + r) * 64 + l];
+                    G[(size_t)q * k + p] = x;
+                    G[(size_t)p * k + q] = x;
+                }
+    const double* tv = v + (size_t)i * 256;
+    for (int x = 0; x < tail; ++x)
+        for (int c = 0; c <= k0 + x; ++c) {
+            G[(size_t)(k0 + x) * k + c] = tv[x * 64 + c];
+            G[(size_t)c * k + (k0 + x)] = tv[x * 64 + c];
+        }
+}
 void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, hipStream_t s) {
     const int nb = gram_blocks(a.ntiles), nv = gram_values(k);
     double* P = scratch;
     double* Q = P + (size_t)nb * nv;
     double* out = Q + (size_t)64 * nv;
-    if (k <= 32)
-        hipLaunchKernelGGL(k_gram<1>, dim3(nb), dim3(256), 0, s, F, a, f, k, P);
-    else
-        hipLaunchKernelGGL(k_gram<2>, dim3(nb), dim3(256), 0, s, F, a, f, k, P);
+    int nc16, tail;
+    gram_config(k, nc16, tail);
+#define TK_GRAM_CASE(A_, B_)                                                                       \
+    if (nc16 == A_ && tail == B_) hipLaunchKernelGGL((k_gram<A_, B_>), dim3(nb), dim3(256), 0, s, F, a, f, k, P);
+    TK_GRAM_CASE(0, 0) TK_GRAM_CASE(0, 1) TK_GRAM_CASE(0, 2) TK_GRAM_CASE(0, 3) TK_GRAM_CASE(0, 4)
+    TK_GRAM_CASE(1, 0) TK_GRAM_CASE(1, 1) TK_GRAM_CASE(1, 2) TK_GRAM_CASE(1, 3) TK_GRAM_CASE(1, 4)
+    TK_GRAM_CASE(2, 0)
+#undef TK_GRAM_CASE
     // two fixed-order levels: segments of 16 partials, then the segment sums
     const int seg = 16, nseg = (nb + seg - 1) / seg;
     hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 255) / 256, nseg), dim3(256), 0, s, P, nb, nv, seg, Q);

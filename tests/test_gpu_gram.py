@@ -4,8 +4,9 @@ src/tensor_krylov_method.jl:103).
 
 G = V[:, :k]' V[:, :k] on v_mfma_f64_16x16x4f64 must equal the host product of the basis the
 device holds (entries are O(1) on the diagonal and O(eps) off it: absolute 1e-14 at n = 5000,
-1e-13 at n = 2^20, where each entry sums 2^20 products); k crosses the 32-column block edge
-and odd k exercises the masked last column of a pair.  The driver's orthogonality_data with
+1e-13 at n = 2^20, where each entry sums 2^20 products); k covers every column-group layout
+(even/odd groups, 16-column runs, a tail of 1..4 columns on the VALU) and odd k exercises the
+masked last column of a pair.  The driver's orthogonality_data with
 a deferred Gram (TensorLanczos' default) must be rounding noise of the same size as with a
 Gram row per step, and the rest of the trajectory bitwise the same (TensorArnoldi) or equal to
 rounding (TensorLanczos, whose gram-free step is another kernel, k_lan_1w).
@@ -24,7 +25,7 @@ def _tk():
 @pytest.mark.parametrize("method", [0, 1])
 def test_gram_matches_host_product(ctx, method):
     tk = _tk()
-    n, K, d = 5000, 50, 2
+    n, K, d = 5000, 63, 2
     csc = tk.assemble_matrix(n, "Laplace")
     rng = np.random.default_rng(21)
     bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
@@ -32,7 +33,9 @@ def test_gram_matches_host_product(ctx, method):
     dev = tk.DeviceDecomposition(ctx, method, d, 0, [A] * d, bs, K)
     dev.init(False)
     dev.sweep(0, K)
-    for k in (1, 2, 7, 31, 32, 33, 50, 51):
+    # every column-group layout of k_gram: even/odd groups only (k <= 32), a VALU tail of
+    # 1..4 columns (33..36, 49..52), a padded 16-column group (37..48, 53..64)
+    for k in (1, 2, 7, 31, 32, 33, 34, 35, 36, 37, 40, 47, 48, 49, 50, 51, 52, 53, 63, 64):
         G = dev.gram(1, k)
         V = dev.basis(1, 0, k)
         ref = V.T @ V

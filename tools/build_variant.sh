@@ -8,7 +8,7 @@ mkdir -p $R/tools/_build
 src=$R
 if [ "$rev" != "-" ]; then
   src=$(mktemp -d)
-  for f in include/tk.h tensorkrylov.jl_amd/csrc/tk_kernels.hip tensorkrylov.jl_amd/csrc/tk_abi.cpp tensorkrylov.jl_amd/csrc/tk_host.cpp tensorkrylov.jl_amd/csrc/tk_host.h tensorkrylov.jl_amd/csrc/tk_solver.cpp tensorkrylov.jl_amd/csrc/tk_internal.h; do
+  for f in include/tk.h tensorkrylov.jl_amd/csrc/tk_kernels.hip tensorkrylov.jl_amd/csrc/tk_abi.cpp tensorkrylov.jl_amd/csrc/tk_host.cpp tensorkrylov.jl_amd/csrc/tk_host.h tensorkrylov.jl_amd/csrc/tk_solver.cpp tensorkrylov.jl_amd/csrc/tk_internal.h tensorkrylov.jl_amd/csrc/tk_xsched.h; do
     mkdir -p $src/$(dirname $f); git -C $R show $rev:$f > $src/$f 2>/dev/null || rm -f $src/$f
   done
 fi
