@@ -1743,9 +1743,17 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         if (st) return st;
     }
     if (!dc->gram_scr) HIPCHK(hipMalloc((void**)&dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double)));
-    // on the Gram stream after everything enqueued so far (the steps that wrote columns < k)
-    hipStream_t s = c->gstream;
-    {
+    // after everything enqueued so far (the steps that wrote columns < k): on the compute
+    // stream itself by default -- run beside the end-of-solve V*Y the two kernels took longer
+    // together than one after the other, and the two cross-stream event hand-offs of the side
+    // stream cost the tracked factor's rank ~100 us per solve at one factor per GPU
+    // (TKHIP_GRAM_STREAM=side keeps the side stream for experiments)
+    static const bool side = [] {
+        const char* e = getenv("TKHIP_GRAM_STREAM");
+        return e && !strcmp(e, "side");
+    }();
+    hipStream_t s = side ? c->gstream : c->stream;
+    if (side) {
         HIPCHK(hipEventRecord(dc->gev_in, c->stream));
         HIPCHK(hipStreamWaitEvent(s, dc->gev_in, 0));
     }
@@ -1755,8 +1763,10 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         launch_gram(dc->df, f, a, k, dc->gram_scr, s);
     }
     LAUNCHCHK("gram");
-    HIPCHK(hipEventRecord(dc->gev_done, s));
-    dc->gram_inflight = true;
+    if (side) {
+        HIPCHK(hipEventRecord(dc->gev_done, s));
+        dc->gram_inflight = true;
+    }
     if (!G) return TK_OK;
     const int nv = gram_values(k);
     std::vector<double> vbuf;

@@ -2528,15 +2528,26 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
     }
 }
 
-// out[s][v] = sum over partials b in [s*seg, min(nb, (s+1)*seg)) of P[b][v], in b order
-__global__ __launch_bounds__(256) void k_gram_reduce(const double* __restrict__ P, int nb, int nv, int seg,
+// out[v] = sum over the nb block partials P[b][v] in one launch: 32 threads per value, thread s
+// summing partials [s*seg, (s+1)*seg) in order, then the 32 segment sums in order (fixed order
+// for a given nb, so bitwise reproducible); 8 values per block, lanes of a value group read
+// 8 consecutive values of one partial row
+__global__ __launch_bounds__(256) void k_gram_reduce(const double* __restrict__ P, int nb, int nv,
                                                      double* __restrict__ out) {
-    const int v = blockIdx.x * 256 + threadIdx.x;
-    if (v >= nv) return;
-    const int b0 = blockIdx.y * seg, b1 = min(nb, b0 + seg);
+    __shared__ double ss[32][8];
+    const int vv = threadIdx.x & 7, sg = threadIdx.x >> 3;
+    const int v = blockIdx.x * 8 + vv;
+    const int seg = (nb + 31) / 32, b0 = sg * seg, b1 = min(nb, b0 + seg);
     double s = 0.0;
-    for (int b = b0; b < b1; ++b) s += ld(P, (int64_t)b * nv + v);
-    st(out, (int64_t)blockIdx.y * nv + v, s);
+    if (v < nv)
+        for (int b = b0; b < b1; ++b) s += ld(P, (int64_t)b * nv + v);
+    ss[sg][vv] = s;
+    __syncthreads();
+    if (sg == 0 && v < nv) {
+        double r = 0.0;
+        for (int q = 0; q < 32; ++q) r += ss[q][vv];
+        st(out, v, r);
+    }
 }
 
 // ------------------------------------------------------------------ plain SpMV (test hook)
@@ -2869,10 +2880,8 @@ void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, h
     TK_GRAM_CASE(1, 0) TK_GRAM_CASE(1, 1) TK_GRAM_CASE(1, 2) TK_GRAM_CASE(1, 3) TK_GRAM_CASE(1, 4)
     TK_GRAM_CASE(2, 0)
 #undef TK_GRAM_CASE
-    // two fixed-order levels: segments of 16 partials, then the segment sums
-    const int seg = 16, nseg = (nb + seg - 1) / seg;
-    hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 255) / 256, nseg), dim3(256), 0, s, P, nb, nv, seg, Q);
-    hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 255) / 256, 1), dim3(256), 0, s, Q, nseg, nv, nseg, out);
+    (void)Q;
+    hipLaunchKernelGGL(k_gram_reduce, dim3((nv + 7) / 8), dim3(256), 0, s, P, nb, nv, out);
 }
 
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
