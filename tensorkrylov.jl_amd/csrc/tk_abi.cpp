@@ -1388,7 +1388,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             tk_status st2 = bk_flush(dc);
             if (st2) return st2;
         }
-        RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, s), "arn_d1");
+        RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, s), "arn_d1");
         // (its last block per factor also evaluates the next step's scalars)
         if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
         dc->bk_j = j;

@@ -254,10 +254,11 @@ struct Row {
     // column checks, and `last` is one of their columns.
     // loadm for an even nc: whole pairs only, no selects on the loaded values (a uniform
     // select there made the compiler wait for the row before its next loads); `last` unset
+    template <int PLO = 0>   // pairs below PLO are not loaded (k_arn_d1 keeps them in LDS)
     __device__ __forceinline__ void loadm_even(rsrc_t basis, uint32_t toff, int nc) {
         constexpr int P0 = MAXC / 2 - 4;
 #pragma unroll
-        for (int p = 0; p < MAXC / 2; ++p) {
+        for (int p = PLO; p < MAXC / 2; ++p) {
             const uint32_t off = (p < P0 || 2 * p < nc) ? toff + (uint32_t)p * (TPB * 16) : 0x80000000u;
             const d2_t x = bld2(basis, off);
             v[2 * p] = x.x;
@@ -355,6 +356,43 @@ __device__ __forceinline__ void row_dot2(const Row<MAXC>& R, const double* __res
             a1 += R.v[c + 1] * CP4(hh)[c + 1];
             b0 += R.v[c] * CP4(gg)[c];
             b1 += R.v[c + 1] * CP4(gg)[c + 1];
+        }
+    }
+    sh = a0 + a1;
+    sg = b0 + b1;
+}
+// Same, with columns c < LC read from LDS (pair p of this thread's row at vl[p * TPB + t], zero
+// for rows outside the basis) as each chunk of 8 is reached: the same order, so bitwise equal.
+template <int MAXC, int LC>
+__device__ __forceinline__ void row_dot2_lc(const Row<MAXC>& R, const d2_t* vl, int t, bool inb,
+                                            const double* __restrict__ h, const double* __restrict__ g,
+                                            double& sh, double& sg) {
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    uint64_t ph = (uint64_t)h, pg = (uint64_t)g;
+#pragma unroll
+    for (int c0 = 0; c0 < MAXC; c0 += 8) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+s"(ph), "+s"(pg) : "v"(a0), "v"(b0));
+        const double* hh = (const double*)ph;
+        const double* gg = (const double*)pg;
+        double cv[8];
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            if (c0 + i < LC) {
+                const d2_t x = vl[((c0 + i) >> 1) * TPB + t];
+                cv[i] = inb ? x.x : 0.0;
+                cv[i + 1] = inb ? x.y : 0.0;
+            } else {
+                cv[i] = R.v[c0 + i < MAXC ? c0 + i : 0];
+                cv[i + 1] = R.v[c0 + i + 1 < MAXC ? c0 + i + 1 : 0];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i += 2) {
+            a0 += cv[i] * CP4(hh)[c0 + i];
+            a1 += cv[i + 1] * CP4(hh)[c0 + i + 1];
+            b0 += cv[i] * CP4(gg)[c0 + i];
+            b1 += cv[i + 1] * CP4(gg)[c0 + i + 1];
         }
     }
     sh = a0 + a1;
@@ -868,6 +906,20 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_RS64
 #define TK_D1_RS64 1
 #endif
+// Register rows of at least TK_D1_LCMIN columns keep their lowest TK_D1_LC columns in LDS,
+// loaded there directly (buffer_load ... lds, no VGPR destination) and read back as each use
+// comes: the register budget of a row TK_D1_LC columns narrower -- one wave per SIMD more,
+// so more rows' loads in flight per CU -- for 32 KB of LDS per block (0 = all in registers)
+#ifndef TK_D1_LC
+#define TK_D1_LC 0   // measured 2.6 % slower at 16 (profiles/r03/d1_ldscols_ab.txt): off
+#endif
+#ifndef TK_D1_LCMIN
+#define TK_D1_LCMIN 48
+#endif
+#ifndef TK_D1_LCMAX
+#define TK_D1_LCMAX 48   // (56 columns with 16 in LDS still spill 22 registers at 4 waves)
+#endif
+#define D1_LCOLS(M) (TK_D1_LC > 0 && TK_D1_RS64 && TK_D1_SWPIN && (M) >= TK_D1_LCMIN && (M) <= TK_D1_LCMAX ? TK_D1_LC : 0)
 #ifndef TK_D1_SWPIN
 #define TK_D1_SWPIN 1
 #endif
@@ -883,10 +935,12 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
         if ((t & 3) == 0) acc[(k) * 64 + (t >> 6) * 16 + ((t >> 2) & 15)] += r_;        \
     } while (0)
 #define D1_NP 4
+#define D1_CHW 64
 #define D1_PART(k, p, sl) acc[(k) * 64 + (p) * 16 + (sl)]
 #else
 #define D1_ACC(k, x) acc[(k) * TPB + t] += rs16(x)
 #define D1_NP 16
+#define D1_CHW TPB
 #define D1_PART(k, p, sl) acc[(k) * TPB + (p) * 16 + (sl)]
 #endif
 #if TK_D1_TRACE
@@ -915,7 +969,10 @@ template <int MAXC, int FMT>
 #if TK_D1_OCCT
 // narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
 #if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
-#define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 16 ? 6 : (MAXC <= 24 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3))))
+// (with TK_D1_LC the top tiers keep their low TK_D1_LC columns in LDS: the register row is
+// TK_D1_LC columns narrower, and so is the tier)
+#define D1_RC (MAXC - D1_LCOLS(MAXC))
+#define D1_OCC (D1_RC <= 8 ? 8 : (D1_RC <= 16 ? 6 : (D1_RC <= 24 ? 5 : (D1_RC <= TK_D1_L4 ? 4 : (D1_RC <= TK_D1_L3 ? 3 : 2)))))
 #else
 #define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
 #endif
@@ -925,7 +982,9 @@ template <int MAXC, int FMT>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a,
                                                                                                   KArgs b) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
-    __shared__ double xs[4][TPB];   // u_j, u_{j+1} by window parity
+    constexpr int LC = D1_LCOLS(MAXC);   // low columns of the row kept in LDS (TK_D1_LC)
+    static_assert(LC % 8 == 0 && (LC == 0 || LC <= MAXC - 8), "LDS columns: whole chunks of 8, below the patched pairs");
+    __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
 #if TK_D1_COEF_LDS
     __shared__ __attribute__((aligned(16))) double cl[2][MAXC];   // c, h1
 #endif
@@ -963,7 +1022,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
-    double* acc = lds;
+    // dynamic LDS: [ LDS columns: LC/2 pairs x TPB rows | column-dot slots ]
+    const d2_t* vl = (const d2_t*)lds;
+    double* acc = lds + LC * TPB;
     const int j = a.j, t = threadIdx.x;
     const int hl = d.hl, hu = d.hu, WS = TPB - 2 * (hl + hu);
     const double* Uin = a.ubuf ? d.W : d.U;
@@ -980,7 +1041,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
     const bool gram = d.track_gram != 0;
     const int nch = NUZ + 1 + (gram ? NG : 0);
-    for (int k = 0; k < nch; ++k) acc[k * TPB + t] = 0.0;   // private slots
+    for (int e = t; e < nch * D1_CHW; e += TPB) acc[e] = 0.0;   // private slots
 #if TK_D1_COEF_LDS
     // coefficient entries past the live ones are zero (init) and meet zero or finite
     // basis entries
@@ -1009,7 +1070,16 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // column j-1 from E
         int jl = j & ~1;   // the per-pair conditions are re-derived each window (hoisted: SGPR spills)
         asm volatile("" : "+s"(jl));
-        R.loadm_even(tv, toff, jl);
+        if (LC > 0) {
+            // the low pairs straight into LDS (lane-linear: pair p of row t at vl[p * TPB + t];
+            // rows outside the basis read zero and are masked where read)
+#pragma unroll
+            for (int p = 0; p < LC / 2; ++p)
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    tv, (__attribute__((address_space(3))) void*)(vl + p * TPB + (t & ~63)), 16,
+                    toff + (uint32_t)p * (TPB * 16), 0, 0, 2);
+        }
+        R.template loadm_even<LC / 2>(tv, toff, jl);
         // (both loads issued before the patch below waits for the row)
         const double up = inb ? ld(Uin, r) : 0.0;
         const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
@@ -1022,7 +1092,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #if TK_D1_COEF_LDS
         row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sq);
 #else
-        row_dot2<MAXC>(R, c, qv, sc, sq);
+        if constexpr (LC > 0) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's LDS columns have landed
+            row_dot2_lc<MAXC, LC>(R, vl, t, inb, c, qv, sc, sq);
+        } else {
+            row_dot2<MAXC>(R, c, qv, sc, sq);
+        }
 #endif
         D1_PHASE(0);
         // v_j = (u_j - V c) ib.  With h1 = V'A v_j = (q - Hbar c) ib (CGS's first projection;
@@ -1031,7 +1106,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         //   u_{j+1} = A v_j - V h1[0..j) - h1[j] v_j   into   ib (A u_j - V q) - gamma v_j
         // (the Hbar c terms cancel): the SpMV is applied to u_j itself, no Hbar is needed
         double* xv = xs[par];
-        double* xu = xs[2 + par];
+        double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
         const double vj = ok ? (up - sc) * inv_beta : 0.0;
 #if TK_BK_TEST & 32
         xv[t] = vj;
@@ -1055,7 +1130,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
         // update_rhs!'s <v_j, b> as norm(b) * <v_j, v_0> (b = norm(b) v_0, src/decompositions.jl:
         // 112-118): v_0 is column 0 of the register row, so b is not read (-8 B per row)
-        const double v0r = j > 0 ? R.v[0] : vj;
+#define D1_V0R (j > 0 ? (LC > 0 ? (inb ? vl[t].x : 0.0) : R.v[0]) : vj)   // (read where used)
 #ifndef TK_D1_NORED   // (timing experiment: column dots skipped)
 #if TK_D1_RS64 && TK_D1_SWPIN
         // rs64's first step on the inputs: the basis entries of columns c and c+4 are
@@ -1068,16 +1143,30 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         if (gram) swap32(vo, vo, mv1, mv2);
 #pragma unroll
         for (int g = 0; g < (NUZ + 1) / 2; ++g) {
+            // (with LDS columns: this chunk pair's reads are issued here, not hoisted into
+            // one burst that holds them all in registers)
+            if (LC > 0) __builtin_amdgcn_sched_barrier(0);
             double yg[8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int k = 2 * g + h;
                 if (k < NUZ && 8 * k < j) {
-                    double y[8];
+                    double y[8], c8[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i += 2) {
+                        if (8 * k < LC) {   // (re-read from LDS: the row_dot2 copies are dead)
+                            const d2_t x = vl[(4 * k + (i >> 1)) * TPB + t];
+                            c8[i] = inb ? x.x : 0.0;
+                            c8[i + 1] = inb ? x.y : 0.0;
+                        } else {
+                            c8[i] = R.v[8 * k + i < MAXC ? 8 * k + i : 0];
+                            c8[i + 1] = R.v[8 * k + i + 1 < MAXC ? 8 * k + i + 1 : 0];
+                        }
+                    }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         double vd, vs;
-                        swap32(R.v[8 * k + q], R.v[8 * k + 4 + q], vd, vs);
+                        swap32(c8[q], c8[4 + q], vd, vs);
                         y[2 * q] = fma(vs, mu2, vd * mu1);
                         y[2 * q + 1] = fma(vs, mz2, vd * mz1);
                         yg[4 * h + q] = fma(vs, mv2, vd * mv1);   // 0 unless gram (mv = 0)
@@ -1120,9 +1209,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #if TK_D1_RS64 && TK_D1_SWPIN
             // the six scalars in value slots 0..2 (lower half-wave) and 8..10 (upper): three
             // cross-half exchanges, the rest of the first step is zeros
+            if (LC > 0) __builtin_amdgcn_sched_barrier(0);
+            const double v0r = D1_V0R;
             double y[8] = {swap_add32(vo * u, uo * z), swap_add32(vo * z, vo * v0r), swap_add32(uo * u, vo * vj)};
             D1_ACC_Y(NUZ, y);
 #else
+            const double v0r = D1_V0R;
             double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
             D1_ACC(NUZ, x);
 #endif
@@ -2701,12 +2793,13 @@ void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
         hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
     });
 }
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, hipStream_t s) {
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
-    size_t lds = (size_t)(M / 8 + 1 + (M + 15) / 16) * TPB * sizeof(double);
+    // [ LDS columns (TK_D1_LC) | column-dot slots: (u,z) chunks + scalars (+ Gram chunks) ]
+    size_t lds = ((size_t)D1_LCOLS(M) * TPB + (size_t)(M / 8 + 1 + (gram ? (M + 15) / 16 : 0)) * D1_CHW) * sizeof(double);
     if (b.j >= 0) lds = std::max(lds, bk_lds_doubles(b.j) * sizeof(double));
     const int gx = TK_D1_ONEWIN ? (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
     with_band_fmt(a.fmt, [&](auto FM) {
