@@ -1,0 +1,10 @@
+# factor groups for the Gram-free one-sweep Lanczos too: GPU suite, then C2 TensorLanczos A/B
+set -o pipefail
+R=$GRAFT_REPO_ROOT; cd $R; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_grp2.log 2>&1
+rc=$?; tail -3 gpurun_out/t_grp2.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error" gpurun_out/t_grp2.log | head; exit 1; }
+for rep in 1 2; do for G in 1 2; do
+  TKHIP_FACTOR_GROUPS=$G timeout -k 10 300 python bench.py --method TensorLanczos --steps 8 --warmup 2 --no-cpu-baseline > gpurun_out/grpl_$G.log 2>&1 || { echo "bench TL $G failed"; tail -5 gpurun_out/grpl_$G.log; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('gpurun_out/grpl_$G.log').read().strip().split('\n')[-1]); e=d.get('end_to_end') or {}; print('rep$rep TL groups=$G', d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline'].get('avg_launch_us'), 'e2e', e.get('iterations_s'))"
+done; done
