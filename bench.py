@@ -379,6 +379,10 @@ def main():
                     "reference_algorithm_effective_GBs": round((ref_step / K) / step_avg_s / 1e9, 1)}
                    if method == "TensorArnoldi" and sweeps == 1 and step_cnt else {}),
                 "avg_launch_us": round(step_avg_s * 1e6, 2),
+                # 2: the local factors step as two groups, each in its own launches on its own
+                # stream; avg_launch_us is then the span of a step's two concurrent launch pairs
+                # (rocprofv3 lists each group's k_arn_d1 apart, over half the factors' bytes)
+                "factor_groups": dev.factor_groups if method == "TensorArnoldi" and sweeps == 1 else 1,
             },
             "host_issue_us_per_iteration": round(host_us_per_step, 2),
             "end_to_end": e2e,

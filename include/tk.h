@@ -231,6 +231,13 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G);
  * TK_LANCZOS_REORTH (its loss check drives the redo) and track_all_gram keep rows. */
 int tk_decomp_gram_deferred(tk_decomp* dc);
 
+/* Launch streams of the one-sweep Arnoldi step: 2 when the local factors step as two groups,
+ * each in its own launches on its own stream of the context (one group's launch drain and
+ * reduce overlap the other's sweep), else 1.  Groups apply on a single rank (no records
+ * exchange) with nf >= 2; TKHIP_FACTOR_GROUPS=1 at create keeps one stream.  Results are
+ * bitwise those of one stream (every kernel is per factor). */
+int tk_decomp_factor_groups(tk_decomp* dc);
+
 /* basis_tensor_mul! (src/utils.jl:478-488, called at src/tensor_krylov_method.jl:112):
  * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).
  * Y: host [nf][t][k] (each Y_s column-major k x t).  X: host [nf][t][n] (column-major

@@ -1092,6 +1092,8 @@ int tk_decomp_matrix_reads(tk_decomp* dc) { return !dc ? -1 : (dc->mfspmv ? 1 : 
 
 int tk_decomp_gram_deferred(tk_decomp* dc) { return dc && dc->gram_deferred ? 1 : 0; }
 
+int tk_decomp_factor_groups(tk_decomp* dc) { return dc && dc->g1 > 0 ? 2 : 1; }
+
 tk_status tk_decomp_set_replica(tk_decomp* dc, int replica) { TK_API_BEGIN
     CHECKARG(dc, "NULL handle");
     if (dc->inited) return fail(TK_ERR_STATE, "tk_decomp_set_replica: after tk_decomp_init");

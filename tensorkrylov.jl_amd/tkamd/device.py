@@ -154,6 +154,11 @@ class DeviceDecomposition:
         return int(self.ctx._lib.tk_decomp_matrix_reads(self.h))
 
     @property
+    def factor_groups(self):
+        """Streams the one-sweep Arnoldi step's launches use (tk_decomp_factor_groups)."""
+        return int(self.ctx._lib.tk_decomp_factor_groups(self.h))
+
+    @property
     def gram_deferred(self):
         """Factor 0's Gram comes from one SYRK (gram()) rather than per-step record rows
         (tk_decomp_gram_deferred)."""

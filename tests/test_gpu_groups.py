@@ -1,0 +1,52 @@
+"""One-sweep Arnoldi factor groups (tk_decomp_factor_groups): the local factors step as two
+groups, each in its own launches on its own stream, so one group's launch drain and reduce
+overlap the other's sweep.  Every kernel is per factor, so the records, the basis, the
+flushed column and V*Y must be bitwise those of one stream (TKHIP_FACTOR_GROUPS=1), whether
+the steps are taken one at a time with their records (the driver's pattern) or as a sweep,
+and for an odd factor count (groups of 2 and 3).  Reference: the per-factor steps of
+orthonormalize! (src/orthogonal_bases.jl:162-180) are independent of each other.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("d", [2, 5])
+def test_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
+    import tkamd as tk
+    n, K, t = 3000, 40, 5
+    rng = np.random.default_rng(77)
+    mats = [tk.assemble_matrix(n, "Laplace"), tk.assemble_matrix(n, "ConvDiff")]
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    Ys = [rng.standard_normal((K, t)) for _ in range(d)]
+    out = {}
+    for G in ("1", "2"):
+        monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
+        A = [tk.DeviceMatrix(ctx, m) for m in mats]
+        dev = tk.DeviceDecomposition(ctx, 0, d, 0, [A[s % 2] for s in range(d)], bs, K)
+        assert dev.arnoldi_sweeps == 1
+        assert dev.factor_groups == int(G)
+        r0 = dev.init()
+        recs = [dev.step(j) for j in range(12)]          # one at a time, records read
+        dev.sweep(12, K - 1)                             # the rest as a sweep
+        recs.append(dev.step(K - 1))
+        recs.append(dev.flush())
+        allrec = dev.records(0, K + 1)
+        V = [dev.basis(f, 0, K + 1) for f in range(d)]
+        X = dev.basis_mul(K, Ys)
+        out[G] = (r0, recs, allrec, V, X)
+        dev.close()
+        for a in A:
+            a.close()
+    (a0, ar, aa, aV, aX), (b0, br, ba, bV, bX) = out["1"], out["2"]
+    assert np.array_equal(a0, b0)
+    for x, y in zip(ar, br):
+        assert np.array_equal(x, y)
+    assert np.array_equal(aa, ba)
+    for x, y in zip(aV, bV):
+        assert np.array_equal(x, y)
+    for x, y in zip(aX, bX):
+        assert np.array_equal(x, y)
+    # and the basis is an orthonormal Arnoldi basis
+    assert np.abs(aV[0].T @ aV[0] - np.eye(K + 1)).max() < 1e-12
