@@ -184,8 +184,14 @@ struct Deadline {
     }
 };
 
-// hipStreamSynchronize with a deadline
+// hipStreamSynchronize with a deadline -- only where another rank can be involved: without a
+// communicator (one GPU) queued work of any length is waited for plainly, and never marks the
+// context stuck
 static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int slot = -1) {
+    if (!c->comm) {
+        const hipError_t e = hipStreamSynchronize(s);
+        return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
     Deadline dl;
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
@@ -197,6 +203,10 @@ static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int sl
 
 // hipEventSynchronize with a deadline
 static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int slot = -1) {
+    if (!c->comm) {
+        const hipError_t e = hipEventSynchronize(ev);
+        return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    }
     Deadline dl;
     for (;;) {
         const hipError_t e = hipEventQuery(ev);
@@ -884,7 +894,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->npd = std::max(dc->npd, d.npd);
         d.nwl = lan_windows(n, d.hl, d.hu);
         dc->nwl = std::max(dc->nwl, d.nwl);
-        const int npp = std::max(std::max(dc->npart, dc->onesweep ? d.npd : 0), dc->ntiles);
+        // partial slots: CGS2 (npart), one-sweep Arnoldi windows (npd), k_lan_1w's wide windows
+        // (nwl: more than ntiles when TK_LAN_RPT = 1 and the band is wide), one per tile (k_fin_d)
+        const int npp = std::max(std::max(std::max(dc->npart, dc->onesweep ? d.npd : 0), dc->onesweep ? d.nwl : 0),
+                                 dc->ntiles);
         DA(d.V, (size_t)dc->ntiles * 256 * ((kmax + 2) & ~1) * sizeof(double));   // tile-major, paired columns
         double* bb;
         DA(bb, (size_t)dc->ld * sizeof(double));
@@ -1057,25 +1070,28 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     if (dc->recv != dc->rec && c->nranks > 1) {
         // preflight: every rank must describe the same decomposition, and the exchange group
         // size is agreed (max) -- the all-reduce sequence must not depend on one rank's env
-        const char* names[5] = {"d_total", "kmax", "method", "n", "record length"};
-        double v[6] = {(double)d_total, (double)kmax, (double)method, (double)n, (double)dc->m, (double)dc->xs.group};
-        double b[12];
-        for (int i = 0; i < 6; ++i) {
+        // (the Gram mode decides whether every rank's driver joins the orthogonality
+        // all-reduce at the end -- TKHIP_GRAM is read per process, so it is checked here)
+        const char* names[6] = {"d_total", "kmax", "method", "n", "record length", "the Gram mode (TKHIP_GRAM)"};
+        double v[7] = {(double)d_total, (double)kmax, (double)method, (double)n, (double)dc->m,
+                       dc->gram_deferred ? 1.0 : 0.0, (double)dc->xs.group};
+        double b[14];
+        for (int i = 0; i < 7; ++i) {
             b[i] = v[i];
-            b[6 + i] = -v[i];
+            b[7 + i] = -v[i];
         }
-        st = host_allreduce(c, b, 12, ncclMax, "tk_decomp_create preflight");
+        st = host_allreduce(c, b, 14, ncclMax, "tk_decomp_create preflight");
         if (st) {
             free_decomp(dc);
             return st;
         }
-        for (int i = 0; i < 5; ++i)
-            if (b[i] != -b[6 + i]) {
+        for (int i = 0; i < 6; ++i)
+            if (b[i] != -b[7 + i]) {
                 free_decomp(dc);
                 return fail(TK_ERR_ARG, "tk_decomp_create: the %d ranks disagree on %s (min %.17g, max %.17g)",
-                            c->nranks, names[i], -b[6 + i], b[i]);
+                            c->nranks, names[i], -b[7 + i], b[i]);
             }
-        dc->xs.group = (int)b[5];
+        dc->xs.group = (int)b[6];
     }
     c->refs++;
     for (tk_mat* A : dc->mats) A->refs++;
@@ -1718,7 +1734,8 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
                             return fail(TK_ERR_HIP, "waiting for step records: %s", hipGetErrorString(e));
                         if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)
                             return fail(TK_ERR_STATE, "step records of slot %d never arrived", sl);
-                        if (dl.elapsed() > dl.lim)
+                        // (a deadline only where a peer could hold the queue back)
+                        if (c->comm && dl.elapsed() > dl.lim)
                             return fail(TK_ERR_HIP, "step records of slot %d: not complete after %.0f s", sl, dl.lim);
                     }
                 }
@@ -1789,6 +1806,10 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     if (dc->pending && nc > 0 && c0 + nc - 1 >= dc->last_j + (in_e ? 0 : 1)) {
+        // (as tk_decomp_gram: a one-rank read must not start collectives its peers do not join)
+        if (dc->recv != dc->rec && dc->ctx->nranks > 1)
+            return fail(TK_ERR_STATE, "tk_decomp_get_basis: column %d is pending; call tk_decomp_flush on every rank first",
+                        dc->last_j + 1);
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;
     }
@@ -1824,6 +1845,12 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     if (dc->pending && k - 1 >= dc->last_j + (in_e ? 0 : 1)) {
+        // the flush starts record all-reduces (need_slots, the flush slot): with peers, only a
+        // call every rank makes may start them, and the Gram is one rank's -- the caller
+        // flushes on every rank first (tkamd.solver._fill_deferred_orthogonality)
+        if (dc->recv != dc->rec && c->nranks > 1)
+            return fail(TK_ERR_STATE, "tk_decomp_gram: column %d is pending; call tk_decomp_flush on every rank first",
+                        dc->last_j + 1);
         tk_status st = tk_decomp_flush(dc, nullptr);
         if (st) return st;
     }
@@ -1870,7 +1897,8 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
                     return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
                 if (e == hipSuccess && __atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want)
                     return fail(TK_ERR_STATE, "tk_decomp_gram: the result never arrived");
-                if (dl.elapsed() > dl.lim) return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
+                if (c->comm && dl.elapsed() > dl.lim)
+                    return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
             }
         }
     } else {

@@ -106,6 +106,9 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             except CompressedNormBreakdown:                         # :85-96
                 if verbose:
                     print("Early termination at k = %d due to compressed norm breakdown" % k)
+                # orthogonality_data[2..k-1] was filled on the iterations before the breakdown
+                # (:103, then :90-94)
+                _fill_deferred_orthogonality(conv, td, k - 1)
                 conv.niterations = k - 1
                 conv.resize(k - 1)
                 conv.timing["loop_s"] = time.perf_counter() - t_loop
@@ -153,11 +156,17 @@ def _fill_deferred_orthogonality(conv, td, k_last):
     t0 = time.perf_counter()
     part = td.part
     orth = np.zeros(k_last)
+    if part.nranks > 1:
+        # a pending column is written by a flush, whose record all-reduces every rank must
+        # join: all ranks flush here, before the one rank's Gram (tk_decomp_gram refuses to
+        # start collectives on a multi-rank handle)
+        td.dev.flush(False)
     if part.first == 0 and part.nf > 0 and not part.replica:
         G = td.dev.gram(0, k_last)
         orth[:] = orthogonality_losses_from_gram(G)
     if part.nranks > 1:
-        orth = td.ctx.allreduce_host(orth)
+        # (the context's RCCL all-reduce; a backend without a context brings its own)
+        orth = (td.ctx if td.ctx is not None else td.dev).allreduce_host(orth)
     conv.orthogonality_data[1:k_last] = orth[1:k_last]
     conv.timing["orth_gram_s"] = time.perf_counter() - t0
 

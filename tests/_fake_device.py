@@ -23,6 +23,20 @@ class FakeDecomposition:
         self.b = {s: np.asarray(b[s], dtype=np.float64) for s in self.loc}
         self.f = {s: O.Factor(td.A[s], self.b[s], td.kmax) for s in self.loc}
         self.replica = False
+        # TK_FAKE_GRAM_DEFERRED=1: orthogonality_data from one Gram at the end (tk_decomp_gram),
+        # with the ABI's rule that a multi-rank handle refuses a Gram while a column is pending
+        # (the flush that would write it starts record all-reduces every rank must join)
+        import os
+        self.gram_deferred = os.environ.get("TK_FAKE_GRAM_DEFERRED") == "1"
+        self.pending = False
+        self.log = []
+
+    def _world(self):
+        import sys
+        if "torch.distributed" not in sys.modules:
+            return 1
+        import torch.distributed as dist
+        return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
     def set_replica(self):
         self.replica = True
@@ -84,15 +98,32 @@ class FakeDecomposition:
                 r[s, lay.flag] = 1.0 if re else 0.0
                 self._gram(r, s, j + 1)
             r[s, lay.beta] = f.H[j + 1, j]
+        self.pending = True
         return self._exchange(r)
 
     def flush(self, want=True):
+        # the flush slot's records all-reduce (tk_decomp_flush), on every rank alike
+        if self.pending:
+            self.log.append("flush")
+            self._exchange(np.zeros((self.d, self.m)))
+            self.pending = False
         return np.zeros((self.d, self.m))
+
+    def allreduce_host(self, x):
+        return self._exchange(np.asarray(x, dtype=np.float64))
+
+    def gram(self, f, k, want=True):
+        if self.pending and self._world() > 1:
+            raise RuntimeError("tk_decomp_gram: column pending; call tk_decomp_flush on every rank first")
+        self.log.append("gram")
+        V = self.f[self.loc[f]].V[:, :k]
+        return V.T @ V
 
     def basis(self, f, c0, nc):
         return self.f[self.loc[f]].V[:, c0:c0 + nc].copy()
 
     def basis_mul(self, k, Ys, want=True):
+        self.flush(False)   # (tk_decomp_basis_mul finalizes a pending column first)
         return [self.f[s].V[:, :k] @ Ys[i] for i, s in enumerate(self.loc)]
 
     def close(self):

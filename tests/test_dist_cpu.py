@@ -39,9 +39,9 @@ def _single(method, d, K, n=200, tol=1e-9, want_x=False, shared=False):
     return (conv, x) if want_x else conv
 
 
-def _launch(tmp_path, world, method, d, K, *extra):
+def _launch(tmp_path, world, method, d, K, *extra, env_extra=None):
     out = str(tmp_path / "res")
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", **(env_extra or {}))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(HERE, "dist", "worker.py"), out, method, str(d), str(K)] + [str(e) for e in extra]
@@ -115,3 +115,21 @@ def test_term_split_replicas_equal_single_process(tmp_path, world, method, d):
                 assert np.abs(X - xref.fmat[s][:, c0:c1]).max() <= 1e-14 * np.abs(xref.fmat[s]).max()
             cols[c0:c1] += 1
         assert (cols == 0).all()         # every term exactly once
+
+
+@pytest.mark.parametrize("method,K", [("TensorArnoldi", 21), ("TensorLanczos", 20)])
+def test_deferred_gram_multirank_no_convergence(tmp_path, monkeypatch, method, K):
+    """with a deferred Gram and no convergence the driver ends with factor 1's
+    Gram on ONE rank.  A pending column must be flushed by every rank first -- the flush starts
+    record all-reduces, and the ABI (and this stand-in) refuse a Gram on a multi-rank handle
+    while a column is pending.  Odd and even nmax, tolerance never met: the orthogonality data
+    equal the single process' bit for bit."""
+    monkeypatch.setenv("TK_FAKE_GRAM_DEFERRED", "1")
+    res = _launch(tmp_path, 2, method, 4, K, 60, 1e-10, env_extra={"TK_FAKE_GRAM_DEFERRED": "1"})
+    ref = _single(method, 4, K, n=60, tol=1e-10)
+    assert ref.niterations == K
+    for rr in res:
+        assert rr["niter"] == ref.niterations
+        assert np.array_equal(rr["relres"], ref.relative_residual_norm)
+        assert np.array_equal(rr["orth"], ref.orthogonality_data)
+        assert np.count_nonzero(rr["orth"][1:]) == K - 1

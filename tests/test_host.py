@@ -460,3 +460,33 @@ def test_orthogonality_losses_from_one_gram():
     b = np.array([orthogonality_loss_from_gram(G, k) for k in range(1, 41)])
     assert np.allclose(a, b, rtol=1e-12, atol=0)
     assert np.allclose(a, [np.linalg.norm(V[:, :k].T @ V[:, :k] - np.eye(k)) for k in range(1, 41)], rtol=1e-6)
+
+
+def test_deferred_orthogonality_after_breakdown(monkeypatch):
+    """a CompressedNormBreakdown at iteration k ends the Python loop with
+    orthogonality_data[2..k-1] filled, as the reference fills it on every iteration before the
+    breakdown (src/tensor_krylov_method.jl:103, then :85-96) -- also with a deferred Gram."""
+    import tkamd.solver as S
+    from _fake_device import backend
+    monkeypatch.setenv("TK_FAKE_GRAM_DEFERRED", "1")
+    d, n, K, kb = 3, 80, 12, 7
+    A = tkamd.KroneckerMatrix.gallery(tkamd.SymInstance, d, n, tkamd.Laplace)
+    rng = np.random.default_rng(3)
+    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    full = tkamd.ConvergenceData(K)
+    tkamd.tensorkrylov(full, A, [x.copy() for x in b], 1e-10, K, "TensorArnoldi", backend=backend, native=False)
+    real = S.residualnorm
+
+    def breaks(Hm, lam, Ys, k, *a):
+        if k == kb:
+            raise tkamd.CompressedNormBreakdown(-1.0)
+        return real(Hm, lam, Ys, k, *a)
+
+    monkeypatch.setattr(S, "residualnorm", breaks)
+    conv = tkamd.ConvergenceData(K)
+    tkamd.tensorkrylov(conv, A, [x.copy() for x in b], 1e-10, K, "TensorArnoldi", backend=backend, native=False)
+    assert conv.niterations == kb - 1
+    o = np.asarray(conv.orthogonality_data)
+    assert len(o) == kb - 1
+    assert np.all(o[1:] > 0)
+    assert np.array_equal(o[1:], np.asarray(full.orthogonality_data)[1:kb - 1])
