@@ -1009,8 +1009,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     }
     dc->slot_seq.assign(kmax + 2, 0);
     {
+        // with a records exchange the groups need the signal word: the exchange of a step's
+        // slot then waits for the count both groups' bookkeeping blocks add (an event marker
+        // would sit in one group's stream only), and every slot guard is waited for on both
+        // group streams (slot_guard)
         const char* eg = getenv("TKHIP_FACTOR_GROUPS");
-        if (dc->recv == dc->rec && method == TK_ARNOLDI && dc->onesweep && nf >= 2 && !(eg && eg[0] == '1') &&
+        if ((dc->recv == dc->rec || dc->xflag) && method == TK_ARNOLDI && dc->onesweep && nf >= 2 && !(eg && eg[0] == '1') &&
             hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess &&
             hipEventCreateWithFlags(&dc->fev_join, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess)
             dc->g1 = nf / 2;
@@ -1170,8 +1174,12 @@ tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
     // (an already completed exchange needs no wait packet in the compute queue)
-    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess)
+    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess) {
         HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
+        // factor groups already forked: the second group's launches write their factors' rows
+        // of the slot from the other stream (a fork after this point inherits the wait)
+        if (dc->forked) HIPCHK(hipStreamWaitEvent(dc->ctx->fstream, dc->ev_x[dc->xev[slot]], 0));
+    }
     return TK_OK;
 }
 

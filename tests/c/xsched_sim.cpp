@@ -177,6 +177,14 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
     }
     tk_solver_destroy(sv);
     if (outcome == 1) flush(&dc);   // basis_mul's flush of the pending column
+    // the deferred orthogonality Gram (tkamd.solver._fill_deferred_orthogonality):
+    // every rank flushes, then the rank owning factor 1 runs the Gram, which must start no
+    // collective -- tk_decomp_gram refuses a pending column on a multi-rank handle
+    flush(&dc);
+    if (dc.pending) {
+        fprintf(stderr, "rank %d: Gram with column %d pending\n", g_rank, dc.jnext);
+        exit(4);
+    }
     char b[64];
     snprintf(b, sizeof b, "end k=%d outcome=%d", k_end, outcome);
     dc.log.push_back(b);
@@ -218,6 +226,8 @@ int main() {
     bad += run_job("group-env", {{ONESWEEP, 4, 2, 4}, {CGS2, 4, 2, 8}, {EMPTY, 2, 2, 1}}, K, d, 0.0);
     bad += run_job("converged", {{ONESWEEP, 4, 2, 4}, {EMPTY, 8, 3, 4}, {CGS2, 1, 2, 16}}, K, d, 1.0);
     bad += run_job("group1", {{ONESWEEP, 2, 2, 1}, {CGS2, 2, 2, 1}}, 12, 3, 0.0);
+    // odd nmax, no convergence: the last one-sweep step leaves its column pending
+    bad += run_job("odd-nonconv", {{ONESWEEP, 4, 2, 4}, {ONESWEEP, 2, 3, 4}, {EMPTY, 4, 2, 4}}, 49, d, 0.0);
     bad += run_job("mixed8", {{ONESWEEP, 8, 2, 4}, {ONESWEEP, 8, 2, 4}, {CGS2, 8, 2, 4}, {EMPTY, 8, 2, 4},
                               {ONESWEEP, 1, 9, 4}, {CGS2, 2, 2, 4}, {EMPTY, 5, 2, 2}, {ONESWEEP, 3, 4, 7}},
                    K, d, 0.0);

@@ -50,3 +50,55 @@ def test_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
         assert np.array_equal(x, y)
     # and the basis is an orthonormal Arnoldi basis
     assert np.abs(aV[0].T @ aV[0] - np.eye(K + 1)).max() < 1e-12
+
+
+@pytest.mark.parametrize("grp", ["1", "4"])
+def test_factor_groups_under_records_exchange(ctx, grp, monkeypatch):
+    """A rank holding several factors under a records exchange (C4 at 8 GPUs, C2 at 2 and 4):
+    the two group streams signal the exchange through one word and every slot guard is waited
+    for on both.  On a 1-rank communicator (the exchange path, TKHIP_EXCHANGE_ALWAYS) the
+    grouped handle's records, exchanged records, basis and V*Y equal the one-stream local run
+    bit for bit, for exchange groups of 1 and 4 slots."""
+    import tkamd as tk
+    d, n, K, t = 4, 3000, 30, 4
+    rng = np.random.default_rng(5)
+    mats = [tk.assemble_matrix(n, "Laplace"), tk.assemble_matrix(n, "ConvDiff")]
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    Ys = [rng.standard_normal((K, t)) for _ in range(d)]
+
+    def run(c, G):
+        monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
+        A = [tk.DeviceMatrix(c, m) for m in mats]
+        dev = tk.DeviceDecomposition(c, 0, d, 0, [A[s % 2] for s in range(d)], bs, K)
+        assert dev.factor_groups == int(G)
+        r0 = dev.init()
+        recs = [dev.step(j) for j in range(6)]
+        for j in range(6, 14):
+            dev.step_async(j)
+        recs.append(dev.records(7, 14))
+        dev.sweep(14, K)
+        recs.append(dev.records(0, K + 1))
+        V = [dev.basis(f, 0, K) for f in range(d)]
+        X = dev.basis_mul(K, Ys)
+        recs.append(dev.records(K + 1, K + 2))
+        dev.close()
+        for a in A:
+            a.close()
+        return r0, recs, V, X
+
+    local = run(ctx, "1")
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_XCH_GROUP", grp)
+    try:
+        xch = run(c2, "2")
+    finally:
+        c2.close()
+    assert np.array_equal(local[0], xch[0])
+    for a, b in zip(local[1], xch[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(local[2], xch[2]):
+        assert np.array_equal(a, b)
+    for a, b in zip(local[3], xch[3]):
+        assert np.array_equal(a, b)

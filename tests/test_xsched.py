@@ -38,7 +38,7 @@ def _run(sim, local):
 def test_every_rank_issues_the_same_allreduces(sim):
     p, jobs = _run(sim, local=False)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert len(jobs) == 6
+    assert len(jobs) == 7
     for line in jobs:
         assert "identical=1" in line, line
     # the default group of 4 batches the step slots once the issue depth covers a group
