@@ -15,6 +15,7 @@
 // + implicit QL with Wilkinson shifts; general exponential = Higham's degree-13 Pade with
 // scaling and squaring.  Results agree with the NumPy/SciPy oracle to rounding
 // (tests/test_host.py).
+#include <immintrin.h>
 #include <math.h>
 #include <string.h>
 
@@ -191,54 +192,100 @@ bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q) {
 }
 
 // ------------------------------------------------------------------ general exponential
-static void matmul(int n, const double* A, const double* B, double* C) {
-    for (int j = 0; j < n; ++j) {
-        double* c = C + (size_t)j * n;
-        for (int i = 0; i < n; ++i) c[i] = 0.0;
-        for (int k = 0; k < n; ++k) {
-            const double b = B[(size_t)j * n + k];
-            const double* a = A + (size_t)k * n;
-            for (int i = 0; i < n; ++i) c[i] += a[i] * b;
-        }
-    }
-}
+static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, const double* __restrict B, int ldb,
+                    double* __restrict C, int ldc);
+// C = A B (n x n, column-major): the register-blocked AVX2 kernel below (the plain triple loop
+// ran at ~4 GFMA/s at n = 50, the Pade / squaring products being most of a nonsymmetric
+// iteration's host time at C4)
+static void matmul(int n, const double* A, const double* B, double* C) { gemm_nn(n, n, n, A, n, B, n, C, n); }
 
 static bool lu_solve(int n, Vec& A, Vec& B) {
-    // solve A X = B (n x n each), partial pivoting; B overwritten by X
+    // solve A X = B (n x n each), partial pivoting; B overwritten by X.  Columns are separate
+    // arrays to the compiler (restrict): every inner loop is an axpy it vectorizes.
     std::vector<int> piv(n);
+    double* __restrict Ad = A.data();
     for (int k = 0; k < n; ++k) {
+        double* __restrict ak = Ad + (size_t)k * n;
         int p = k;
         for (int i = k + 1; i < n; ++i)
-            if (fabs(A[(size_t)k * n + i]) > fabs(A[(size_t)k * n + p])) p = i;
-        if (A[(size_t)k * n + p] == 0.0) return false;
+            if (fabs(ak[i]) > fabs(ak[p])) p = i;
+        if (ak[p] == 0.0) return false;
         piv[k] = p;
         if (p != k) {
             for (int j = 0; j < n; ++j) std::swap(A[(size_t)j * n + k], A[(size_t)j * n + p]);
             for (int j = 0; j < n; ++j) std::swap(B[(size_t)j * n + k], B[(size_t)j * n + p]);
         }
-        const double inv = 1.0 / A[(size_t)k * n + k];
-        for (int i = k + 1; i < n; ++i) A[(size_t)k * n + i] *= inv;
+        const double inv = 1.0 / ak[k];
+        for (int i = k + 1; i < n; ++i) ak[i] *= inv;
         for (int j = k + 1; j < n; ++j) {
-            const double a = A[(size_t)j * n + k];
+            double* __restrict aj = Ad + (size_t)j * n;
+            const double a = aj[k];
             if (a != 0.0)
-                for (int i = k + 1; i < n; ++i) A[(size_t)j * n + i] -= A[(size_t)k * n + i] * a;
+                for (int i = k + 1; i < n; ++i) aj[i] -= ak[i] * a;
         }
     }
-    for (int j = 0; j < n; ++j) {
-        double* b = &B[(size_t)j * n];
-        for (int k = 0; k < n; ++k)
-            for (int i = k + 1; i < n; ++i) b[i] -= A[(size_t)k * n + i] * b[k];
-        for (int k = n - 1; k >= 0; --k) {
-            b[k] /= A[(size_t)k * n + k];
-            for (int i = 0; i < k; ++i) b[i] -= A[(size_t)k * n + i] * b[k];
+    // the triangular solves for all n right-hand sides at once on a row-major copy of B:
+    // row updates X[i, :] -= L[i, k] X[k, :] are full-length contiguous axpys
+    Vec T((size_t)n * n);
+    double* __restrict X = T.data();
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) X[(size_t)i * n + j] = B[(size_t)j * n + i];
+    for (int k = 0; k < n; ++k) {
+        const double* __restrict xk = X + (size_t)k * n;
+        const double* __restrict ak = Ad + (size_t)k * n;
+        for (int i = k + 1; i < n; ++i) {
+            const double l = ak[i];
+            if (l == 0.0) continue;
+            double* __restrict xi = X + (size_t)i * n;
+            for (int j = 0; j < n; ++j) xi[j] -= l * xk[j];
         }
     }
+    for (int k = n - 1; k >= 0; --k) {
+        double* __restrict xk = X + (size_t)k * n;
+        const double* __restrict ak = Ad + (size_t)k * n;
+        const double dk = ak[k];
+        for (int j = 0; j < n; ++j) xk[j] /= dk;
+        for (int i = 0; i < k; ++i) {
+            const double u = ak[i];
+            if (u == 0.0) continue;
+            double* __restrict xi = X + (size_t)i * n;
+            for (int j = 0; j < n; ++j) xi[j] -= u * xk[j];
+        }
+    }
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i) B[(size_t)j * n + i] = X[(size_t)i * n + j];
     return true;
 }
 
-// exp(A) by Pade approximants of degree 3/5/7/9/13 with scaling and squaring (Higham 2005,
-// the method of Julia's LinearAlgebra.exp!)
-bool expm(int n, const double* A, Vec& E) {
+// exp(c A) by Pade approximants of degree 3/5/7/9/13 with scaling and squaring (Higham 2005,
+// the method of Julia's LinearAlgebra.exp!).  The even powers A^2, A^4, A^6, A^8 of the
+// UNSCALED matrix are formed once (ExpmPowers) and reused by every scalar c: (cA)^2k =
+// c^2k A^2k, so the exponential-sum terms of one iteration, exp(g_j H) for j = 1..t, share
+// them (the products then differ from (cA)(cA) by rounding only).  Scratch in ExpmPowers.
+void ExpmPowers::reset(int n_, const double* A_) {
+    n = n_;
+    A = A_;
+    have = 0;
+    norm1 = 0.0;
+    for (int j = 0; j < n; ++j) {
+        double s = 0.0;
+        for (int i = 0; i < n; ++i) s += fabs(A[(size_t)j * n + i]);
+        norm1 = std::max(norm1, s);
+    }
+    const size_t nn = (size_t)n * n;
+    for (Vec* v : {&U, &V, &T, &Num, &Den}) v->resize(nn);
+}
+
+const double* ExpmPowers::pw(int k) {
+    const size_t nn = (size_t)n * n;
+    if (have < 2) { P2.resize(nn); matmul(n, A, A, P2.data()); have = 2; }
+    if (k >= 4 && have < 4) { P4.resize(nn); matmul(n, P2.data(), P2.data(), P4.data()); have = 4; }
+    if (k >= 6 && have < 6) { P6.resize(nn); matmul(n, P4.data(), P2.data(), P6.data()); have = 6; }
+    if (k >= 8 && have < 8) { P8.resize(nn); matmul(n, P4.data(), P4.data(), P8.data()); have = 8; }
+    return k == 2 ? P2.data() : k == 4 ? P4.data() : k == 6 ? P6.data() : P8.data();
+}
+
+static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
     static const double b13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
                                  1187353796428800.0,  129060195264000.0,   10559470521600.0,
                                  670442572800.0,      33522128640.0,       1323241920.0,
@@ -251,77 +298,80 @@ bool expm(int n, const double* A, Vec& E) {
                                      {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0},
                                      {17643225600.0, 8821612800.0, 2075673600.0, 302702400.0, 30270240.0,
                                       2162160.0, 110880.0, 3960.0, 90.0, 1.0}};
+    const int n = pw.n;
     const size_t nn = (size_t)n * n;
-    double norm1 = 0.0;
-    for (int j = 0; j < n; ++j) {
-        double s = 0.0;
-        for (int i = 0; i < n; ++i) s += fabs(A[(size_t)j * n + i]);
-        norm1 = std::max(norm1, s);
-    }
-    Vec Id(nn, 0.0);
-    for (int i = 0; i < n; ++i) Id[(size_t)i * n + i] = 1.0;
-    Vec U(nn), V(nn), A2(nn);
-    matmul(n, A, A, A2.data());
+    const double* A = pw.A;
+    const double norm1 = fabs(c) * pw.norm1;
+    double* U = pw.U.data();
+    double* V = pw.V.data();
+    double* T = pw.T.data();
     static const int degs[] = {3, 5, 7, 9};
-    for (int q = 0; q < 4; ++q) {
+    int m = 13, s = 0;
+    for (int q = 0; q < 4; ++q)
         if (norm1 <= theta[q]) {
-            const int m = degs[q];
-            const double* b = bd[q];
-            Vec P(Id), Ut(nn, 0.0), Vt(nn, 0.0), tmp(nn);
-            // U = A * sum_{odd} b_k A^{k-1},  V = sum_{even} b_k A^k
-            for (size_t i = 0; i < nn; ++i) {
-                Ut[i] = b[1] * P[i];
-                Vt[i] = b[0] * P[i];
-            }
-            for (int k = 2; k <= m; k += 2) {
-                matmul(n, P.data(), A2.data(), tmp.data());
-                P.swap(tmp);
-                for (size_t i = 0; i < nn; ++i) {
-                    Ut[i] += b[k + 1] * P[i];
-                    Vt[i] += b[k] * P[i];
-                }
-            }
-            matmul(n, A, Ut.data(), U.data());
-            Vec Num(nn), Den(nn);
-            for (size_t i = 0; i < nn; ++i) {
-                Num[i] = Vt[i] + U[i];
-                Den[i] = Vt[i] - U[i];
-            }
-            if (!lu_solve(n, Den, Num)) return false;
-            E.swap(Num);
-            return true;
+            m = degs[q];
+            break;
         }
+    if (m < 13) {
+        // U = cA * sum_{odd k} b_k (cA)^{k-1},  V = sum_{even k} b_k (cA)^k
+        const double* b = bd[m == 3 ? 0 : m == 5 ? 1 : m == 7 ? 2 : 3];
+        for (size_t i = 0; i < nn; ++i) T[i] = V[i] = 0.0;
+        for (int i = 0; i < n; ++i) {
+            T[(size_t)i * n + i] = b[1];
+            V[(size_t)i * n + i] = b[0];
+        }
+        double ck = 1.0;
+        for (int k = 2; k <= m - 1; k += 2) {
+            ck *= c * c;
+            const double* P = pw.pw(k);
+            const double bu = b[k + 1] * ck, bv = b[k] * ck;
+            for (size_t i = 0; i < nn; ++i) {
+                T[i] += bu * P[i];
+                V[i] += bv * P[i];
+            }
+        }
+        matmul(n, A, T, U);
+        for (size_t i = 0; i < nn; ++i) U[i] *= c;
+    } else {
+        if (norm1 > theta[4]) s = std::max(0, (int)ceil(log2(norm1 / theta[4])));
+        const double sc = ldexp(c, -s), s2 = sc * sc, s4 = s2 * s2, s6 = s4 * s2;
+        const double* B2 = pw.pw(2);
+        const double* B4 = pw.pw(4);
+        const double* B6 = pw.pw(6);
+        const double* b = b13;
+        // U = As (B6 (b13 B6 + b11 B4 + b9 B2) + b7 B6 + b5 B4 + b3 B2 + b1 I),
+        // V = B6 (b12 B6 + b10 B4 + b8 B2) + b6 B6 + b4 B4 + b2 B2 + b0 I   (B2k = (sc A)^2k)
+        double* W = pw.Num.data();
+        for (size_t i = 0; i < nn; ++i) T[i] = b[13] * s6 * B6[i] + b[11] * s4 * B4[i] + b[9] * s2 * B2[i];
+        matmul(n, B6, T, W);
+        for (size_t i = 0; i < nn; ++i) W[i] = s6 * W[i] + b[7] * s6 * B6[i] + b[5] * s4 * B4[i] + b[3] * s2 * B2[i];
+        for (int i = 0; i < n; ++i) W[(size_t)i * n + i] += b[1];
+        matmul(n, A, W, U);
+        for (size_t i = 0; i < nn; ++i) U[i] *= sc;
+        for (size_t i = 0; i < nn; ++i) T[i] = b[12] * s6 * B6[i] + b[10] * s4 * B4[i] + b[8] * s2 * B2[i];
+        matmul(n, B6, T, V);
+        for (size_t i = 0; i < nn; ++i) V[i] = s6 * V[i] + b[6] * s6 * B6[i] + b[4] * s4 * B4[i] + b[2] * s2 * B2[i];
+        for (int i = 0; i < n; ++i) V[(size_t)i * n + i] += b[0];
     }
-    int s = 0;
-    if (norm1 > theta[4]) s = std::max(0, (int)ceil(log2(norm1 / theta[4])));
-    const double sc = ldexp(1.0, -s);
-    Vec As(nn);
-    for (size_t i = 0; i < nn; ++i) As[i] = A[i] * sc;
-    Vec B2(nn), B4(nn), B6(nn), tmp(nn);
-    matmul(n, As.data(), As.data(), B2.data());
-    matmul(n, B2.data(), B2.data(), B4.data());
-    matmul(n, B4.data(), B2.data(), B6.data());
-    const double* b = b13;
-    for (size_t i = 0; i < nn; ++i) tmp[i] = b[13] * B6[i] + b[11] * B4[i] + b[9] * B2[i];
-    matmul(n, B6.data(), tmp.data(), U.data());
-    for (size_t i = 0; i < nn; ++i) U[i] += b[7] * B6[i] + b[5] * B4[i] + b[3] * B2[i] + b[1] * Id[i];
-    matmul(n, As.data(), U.data(), tmp.data());
-    U.swap(tmp);
-    for (size_t i = 0; i < nn; ++i) tmp[i] = b[12] * B6[i] + b[10] * B4[i] + b[8] * B2[i];
-    matmul(n, B6.data(), tmp.data(), V.data());
-    for (size_t i = 0; i < nn; ++i) V[i] += b[6] * B6[i] + b[4] * B4[i] + b[2] * B2[i] + b[0] * Id[i];
-    Vec Num(nn), Den(nn);
+    Vec& Num = pw.Num;
+    Vec& Den = pw.Den;
     for (size_t i = 0; i < nn; ++i) {
         Num[i] = V[i] + U[i];
         Den[i] = V[i] - U[i];
     }
     if (!lu_solve(n, Den, Num)) return false;
     for (int q = 0; q < s; ++q) {
-        matmul(n, Num.data(), Num.data(), tmp.data());
-        Num.swap(tmp);
+        matmul(n, Num.data(), Num.data(), T);
+        memcpy(Num.data(), T, nn * sizeof(double));
     }
-    E.swap(Num);
+    E.assign(Num.begin(), Num.end());
     return true;
+}
+
+bool expm(int n, const double* A, Vec& E) {
+    ExpmPowers pw;
+    pw.reset(n, A);
+    return expm_scaled(pw, 1.0, E);
 }
 
 
@@ -340,36 +390,73 @@ static inline double dot4(int n, const double* a, const double* b) {
     return (s0 + s1) + (s2 + s3);
 }
 
-// C[0:m, 0:n] = A[0:m, 0:kk] * B[0:kk, 0:n] (column-major; lda, ldb, ldc); register blocks of
-// 8 rows x 4 columns, the inner dimension streamed (vectorized over rows).
+// C[0:m, 0:n] = A[0:m, 0:kk] * B[0:kk, 0:n] (column-major; lda, ldb, ldc): AVX2 register blocks
+// of 8 rows x 4 columns (eight ymm accumulators; each k step two A loads, four broadcasts,
+// eight FMAs), then 4-row and single-row / single-column edges.  Every C entry is one
+// accumulation in k order (a fused multiply-add per term), whatever block it falls in.
 static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, const double* __restrict B, int ldb,
                     double* __restrict C, int ldc) {
     int j0 = 0;
     for (; j0 + 4 <= n; j0 += 4) {
         const double* b0 = B + (size_t)j0 * ldb;
+        const double* b1 = b0 + ldb;
+        const double* b2 = b1 + ldb;
+        const double* b3 = b2 + ldb;
         int i0 = 0;
         for (; i0 + 8 <= m; i0 += 8) {
-            double acc[4][8] = {};
+            __m256d c00 = _mm256_setzero_pd(), c01 = _mm256_setzero_pd(), c10 = _mm256_setzero_pd(),
+                    c11 = _mm256_setzero_pd(), c20 = _mm256_setzero_pd(), c21 = _mm256_setzero_pd(),
+                    c30 = _mm256_setzero_pd(), c31 = _mm256_setzero_pd();
             for (int c = 0; c < kk; ++c) {
                 const double* a = A + (size_t)c * lda + i0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const double bv = b0[(size_t)q * ldb + c];
-#pragma unroll
-                    for (int r = 0; r < 8; ++r) acc[q][r] += a[r] * bv;
-                }
+                const __m256d a0 = _mm256_loadu_pd(a), a1 = _mm256_loadu_pd(a + 4);
+                __m256d bv = _mm256_broadcast_sd(b0 + c);
+                c00 = _mm256_fmadd_pd(a0, bv, c00);
+                c01 = _mm256_fmadd_pd(a1, bv, c01);
+                bv = _mm256_broadcast_sd(b1 + c);
+                c10 = _mm256_fmadd_pd(a0, bv, c10);
+                c11 = _mm256_fmadd_pd(a1, bv, c11);
+                bv = _mm256_broadcast_sd(b2 + c);
+                c20 = _mm256_fmadd_pd(a0, bv, c20);
+                c21 = _mm256_fmadd_pd(a1, bv, c21);
+                bv = _mm256_broadcast_sd(b3 + c);
+                c30 = _mm256_fmadd_pd(a0, bv, c30);
+                c31 = _mm256_fmadd_pd(a1, bv, c31);
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int r = 0; r < 8; ++r) C[(size_t)(j0 + q) * ldc + i0 + r] = acc[q][r];
+            double* cc = C + (size_t)j0 * ldc + i0;
+            _mm256_storeu_pd(cc, c00);
+            _mm256_storeu_pd(cc + 4, c01);
+            _mm256_storeu_pd(cc + ldc, c10);
+            _mm256_storeu_pd(cc + ldc + 4, c11);
+            _mm256_storeu_pd(cc + 2 * (size_t)ldc, c20);
+            _mm256_storeu_pd(cc + 2 * (size_t)ldc + 4, c21);
+            _mm256_storeu_pd(cc + 3 * (size_t)ldc, c30);
+            _mm256_storeu_pd(cc + 3 * (size_t)ldc + 4, c31);
+        }
+        for (; i0 + 4 <= m; i0 += 4) {
+            __m256d c0 = _mm256_setzero_pd(), c1 = _mm256_setzero_pd(), c2 = _mm256_setzero_pd(),
+                    c3 = _mm256_setzero_pd();
+            for (int c = 0; c < kk; ++c) {
+                const __m256d a0 = _mm256_loadu_pd(A + (size_t)c * lda + i0);
+                c0 = _mm256_fmadd_pd(a0, _mm256_broadcast_sd(b0 + c), c0);
+                c1 = _mm256_fmadd_pd(a0, _mm256_broadcast_sd(b1 + c), c1);
+                c2 = _mm256_fmadd_pd(a0, _mm256_broadcast_sd(b2 + c), c2);
+                c3 = _mm256_fmadd_pd(a0, _mm256_broadcast_sd(b3 + c), c3);
+            }
+            double* cc = C + (size_t)j0 * ldc + i0;
+            _mm256_storeu_pd(cc, c0);
+            _mm256_storeu_pd(cc + ldc, c1);
+            _mm256_storeu_pd(cc + 2 * (size_t)ldc, c2);
+            _mm256_storeu_pd(cc + 3 * (size_t)ldc, c3);
         }
         for (; i0 < m; ++i0) {
             double acc[4] = {};
             for (int c = 0; c < kk; ++c) {
                 const double av = A[(size_t)c * lda + i0];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[q] += av * b0[(size_t)q * ldb + c];
+                acc[0] = fma(av, b0[c], acc[0]);
+                acc[1] = fma(av, b1[c], acc[1]);
+                acc[2] = fma(av, b2[c], acc[2]);
+                acc[3] = fma(av, b3[c], acc[3]);
             }
             for (int q = 0; q < 4; ++q) C[(size_t)(j0 + q) * ldc + i0] = acc[q];
         }
@@ -377,11 +464,17 @@ static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, c
     for (; j0 < n; ++j0) {
         const double* bj = B + (size_t)j0 * ldb;
         double* cj = C + (size_t)j0 * ldc;
-        for (int i = 0; i < m; ++i) cj[i] = 0.0;
-        for (int c = 0; c < kk; ++c) {
-            const double* a = A + (size_t)c * lda;
-            const double bv = bj[c];
-            for (int i = 0; i < m; ++i) cj[i] += a[i] * bv;
+        int i0 = 0;
+        for (; i0 + 4 <= m; i0 += 4) {
+            __m256d c0 = _mm256_setzero_pd();
+            for (int c = 0; c < kk; ++c)
+                c0 = _mm256_fmadd_pd(_mm256_loadu_pd(A + (size_t)c * lda + i0), _mm256_broadcast_sd(bj + c), c0);
+            _mm256_storeu_pd(cj + i0, c0);
+        }
+        for (; i0 < m; ++i0) {
+            double acc = 0.0;
+            for (int c = 0; c < kk; ++c) acc = fma(A[(size_t)c * lda + i0], bj[c], acc);
+            cj[i0] = acc;
         }
     }
 }
@@ -435,12 +528,14 @@ bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, co
             }
         gemm_nn(k, t * d, k, Q, k, ws.M.data(), k, Y, k);
     } else {
+        // every term exp(g_j H1) from the same powers of H1 (ExpmPowers)
         ws.G.resize((size_t)k * k);
+        for (int c = 0; c < k; ++c)
+            for (int i = 0; i < k; ++i) ws.G[(size_t)c * k + i] = H1[(size_t)c * ldh + i];
+        ws.pw.reset(k, ws.G.data());
         for (int j = 0; j < t; ++j) {
             const double g = -alpha[j] * inv;
-            for (int c = 0; c < k; ++c)
-                for (int i = 0; i < k; ++i) ws.G[(size_t)c * k + i] = g * H1[(size_t)c * ldh + i];
-            if (!expm(k, ws.G.data(), ws.Ex)) return false;
+            if (!expm_scaled(ws.pw, g, ws.Ex)) return false;
             for (int s = 0; s < d; ++s) {
                 double* y = Y + (size_t)s * k * t + (size_t)j * k;
                 for (int i = 0; i < k; ++i) y[i] = 0.0;

@@ -14,10 +14,24 @@ bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q);
 // exp(A) (n x n column-major): Pade 3/5/7/9/13 with scaling and squaring
 bool expm(int n, const double* A, Vec& E);
 
+// The even powers A^2..A^8 of one unscaled matrix, formed on demand and shared by every
+// exp(c A) of an iteration (tk_host.cpp expm_scaled), plus scratch.
+struct ExpmPowers {
+    int n = -1;
+    const double* A = nullptr;
+    double norm1 = 0.0;
+    int have = 0;                       // highest even power formed (0, 2, 4, 6, 8)
+    Vec P2, P4, P6, P8;
+    Vec U, V, T, Num, Den;              // scratch
+    void reset(int n_, const double* A_);
+    const double* pw(int k);            // A^k, k in {2, 4, 6, 8}
+};
+
 // Scratch of the two functions below (grown on demand, reused across iterations).
 struct Work {
     Vec w, Q, C, E, M, ec, G, Ex;
     Vec Z, Ly, Lz, X, pre, suf;
+    ExpmPowers pw;
 };
 
 // solve_compressed_system (src/tensor_krylov_method.jl:10-34): lambda[j] = omega[j]/lmin and

@@ -2382,41 +2382,61 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 #define YS_STRIDE 72   // LDS row stride of Ys: rows 2*slot apart land 32 banks apart
 #define XS_STRIDE 260  // LDS column stride of the staged X tile: a 64-lane b64 write is 2-way (optimal)
 #define BM_LDS_DOUBLES (64 * YS_STRIDE)   // Ys; the X staging (16 x XS_STRIDE) reuses it
-// One 256-row tile of X_s[:, t0 .. t0+16NG) = V_s[:, 0..k) Y_s on v_mfma_f64_16x16x4f64: wave w
-// owns rows 64w .. 64w+63 (four 16-row groups), 16-column groups q < NG; Y staged in LDS per
-// 64-deep k chunk.  The accumulators go through LDS (16 columns at a time) so each X column
-// is written as 256 contiguous rows (full lines) instead of 32-B pieces.
-template <int NG>
+// One 256-row tile of X_s[:, t0 .. t0+16NG+TL) = V_s[:, 0..k) Y_s: NG 16-column groups on
+// v_mfma_f64_16x16x4f64 (wave w owns rows 64w .. 64w+63, four 16-row groups) and TL <= 4 tail
+// columns on the VALU -- a 16-column MFMA group holding t mod 16 <= 4 live columns would be
+// three-quarters padding (t = 17 at C2: 2.1x the useful MFMAs when padded to 32); Y staged in
+// LDS per 64-deep k chunk.  The k dimension runs in chunks of 8 columns (two MFMAs over one
+// dwordx4 per lane); a last partial chunk of <= 4 columns takes ONE MFMA whose k-slot l>>4 is
+// column kk + (l>>4) (the half of its pair), not two MFMAs over a padded 8 (k = 50: 13 MFMAs
+// per 16 x 16 block instead of 14).  Each tail column: every lane accumulates its k-slots'
+// products, the 4 k-slot lanes of a row are summed at the end (xor 16, xor 32; fixed order).
+// The accumulators go through LDS (16 columns at a time) so each X column is written as 256
+// contiguous rows (full lines) instead of 32-B pieces.
+template <int NG, int TL>
 __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, const double* __restrict__ Y,
                                                double* __restrict__ X, int k, int t, int tile, int t0,
                                                double* Ys) {
+    constexpr int NC = 16 * NG + TL;   // columns of this block
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
     const double* Vt = d.V + (int64_t)tile * TS;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int lr = lane & 15, lk = lane >> 4;
-    const int tn = min(16 * NG, t - t0);
-    f64x4 acc[4][NG];
+    const int tn = min(NC, t - t0);
+    f64x4 acc[4][NG > 0 ? NG : 1];
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int q = 0; q < NG; ++q) acc[s][q] = (f64x4){0.0, 0.0, 0.0, 0.0};
+    double tac[4][TL > 0 ? TL : 1];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int c = 0; c < TL; ++c) tac[s][c] = 0.0;
     for (int k0 = 0; k0 < k; k0 += 64) {
         const int kn = min(64, k - k0);
         __syncthreads();
-        for (int i = threadIdx.x; i < 64 * 16 * NG; i += 256) {
+        for (int i = threadIdx.x; i < 64 * NC; i += 256) {
             const int kk = i & 63, tt = i >> 6;
             Ys[kk * YS_STRIDE + tt] = (kk < kn && tt < tn) ? ld(Y, (int64_t)(t0 + tt) * k + k0 + kk) : 0.0;
         }
         __syncthreads();
         const rsrc_t tv = mkrsrc(Vt + (int64_t)k0 * TPB, vrange(kn));   // k0 is even: pair aligned
-        const int kp = (kn + 7) & ~7;
+        const int kf = kn & ~7;          // full 8-column chunks
+        const int kr = kn - kf;          // the rest: one 4-slot MFMA if <= 4, else a padded chunk
+        const int kp = kr > 4 ? kn : kf;
         for (int kk = 0; kk < kp; kk += 8) {
             const int ka = kk + 2 * lk;   // this lane's first column of the pair
-            double bq0[NG], bq1[NG];
+            double bq0[NG > 0 ? NG : 1], bq1[NG > 0 ? NG : 1], tq0[TL > 0 ? TL : 1], tq1[TL > 0 ? TL : 1];
 #pragma unroll
             for (int q = 0; q < NG; ++q) {
                 bq0[q] = Ys[ka * YS_STRIDE + 16 * q + lr];
                 bq1[q] = Ys[(ka + 1) * YS_STRIDE + 16 * q + lr];
+            }
+#pragma unroll
+            for (int c = 0; c < TL; ++c) {
+                tq0[c] = Ys[ka * YS_STRIDE + 16 * NG + c];
+                tq1[c] = Ys[(ka + 1) * YS_STRIDE + 16 * NG + c];
             }
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
@@ -2429,21 +2449,58 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
 #pragma unroll
                 for (int q = 0; q < NG; ++q)
                     acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bq1[q], acc[s][q], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < TL; ++c) tac[s][c] = fma(a1, tq1[c], fma(av.x, tq0[c], tac[s][c]));
+            }
+        }
+        if (kr > 0 && kr <= 4) {
+            // k-slot lk = column kf + lk (the even or odd half of its pair), masked past kn
+            const int kc = kf + lk;
+            double bq[NG > 0 ? NG : 1], tq[TL > 0 ? TL : 1];
+#pragma unroll
+            for (int q = 0; q < NG; ++q) bq[q] = Ys[kc * YS_STRIDE + 16 * q + lr];
+#pragma unroll
+            for (int c = 0; c < TL; ++c) tq[c] = Ys[kc * YS_STRIDE + 16 * NG + c];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int row = wave * 64 + s * 16 + lr;
+                const d2_t av = bld2(tv, ((uint32_t)(kc >> 1) * TPB + row) * 16u);
+                const double x = kc < kn ? ((lk & 1) ? av.y : av.x) : 0.0;
+#pragma unroll
+                for (int q = 0; q < NG; ++q)
+                    acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, bq[q], acc[s][q], 0, 0, 0);
+#pragma unroll
+                for (int c = 0; c < TL; ++c) tac[s][c] = fma(x, tq[c], tac[s][c]);
             }
         }
     }
+    // the tail columns' k-slot partials of each row, summed over the 4 k-slot lanes
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int c = 0; c < TL; ++c) {
+            tac[s][c] += __shfl_xor(tac[s][c], 16);
+            tac[s][c] += __shfl_xor(tac[s][c], 32);
+        }
     // epilogue: 16 columns at a time through LDS (Xs[c][row], reusing Ys), then every thread
     // writes its row of each column -- a wave covers 512 contiguous bytes per column
     double* Xs = Ys;
     const int64_t r = (int64_t)tile * TPB + threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < NG; ++q) {
+    for (int q = 0; q < NG + (TL > 0 ? 1 : 0); ++q) {
         if (16 * q >= tn) break;
         __syncthreads();
+        if (q < NG) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+            for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) Xs[lr * XS_STRIDE + wave * 64 + s * 16 + lk + 4 * i] = acc[s][q][i];
+                for (int i = 0; i < 4; ++i) Xs[lr * XS_STRIDE + wave * 64 + s * 16 + lk + 4 * i] = acc[s][q < NG ? q : 0][i];
+        } else if (lk == 0) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int c = 0; c < TL; ++c) Xs[c * XS_STRIDE + wave * 64 + s * 16 + lr] = tac[s][c];
+        }
         __syncthreads();
         if (r < a.n) {
             const int cn = min(16, tn - 16 * q);
@@ -2453,14 +2510,16 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
     }
 }
 
-template <int NG>
+// blockIdx.z = column slice: NG MFMA groups per slice, the last slice of the launch also
+// takes the TL tail columns (slices before it are launched with TL = 0, see launch_basis_mul)
+template <int NG, int TL>
 __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
                                                    const double* __restrict__ Yall,
-                                                   double* __restrict__ Xall, int k, int t) {
+                                                   double* __restrict__ Xall, int k, int t, int z0) {
     __shared__ __attribute__((aligned(16))) double Ys[BM_LDS_DOUBLES];
     const int f = blockIdx.y;
-    basis_mul_tile<NG>(F[f], a, Yall + (int64_t)f * k * t, Xall + (int64_t)f * a.ld * t, k, t, blockIdx.x,
-                       blockIdx.z * 16 * NG, Ys);
+    basis_mul_tile<NG, TL>(F[f], a, Yall + (int64_t)f * k * t, Xall + (int64_t)f * a.ld * t, k, t, blockIdx.x,
+                           (z0 + (int)blockIdx.z) * 16 * 2, Ys);
 }
 
 // The pending column's flush (fin_d_tile, MODE 0: Arnoldi) and V * Y of the same tile in one
@@ -2908,11 +2967,24 @@ void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int 
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
-    // NG = 16-column groups per block: t <= 16 -> 1, <= 32 -> 2, else 2 per z-slice
-    if (t <= 16)
-        hipLaunchKernelGGL(k_basis_mul<1>, dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t);
-    else
-        hipLaunchKernelGGL(k_basis_mul<2>, dim3(a.ntiles, nf, (t + 31) / 32), dim3(256), 0, s, F, a, Y, X, k, t);
+    // 16-column MFMA groups; t mod 16 <= 4 leftover columns go to the VALU tail instead of a
+    // padded group.  Slices of 32 columns (blockIdx.z); the last slice holds the rest.
+    int ng = t / 16, tl = t % 16;
+    if (tl > 4) {
+        ++ng;
+        tl = 0;
+    }
+    const int nz = ng > 2 ? (ng - 1) / 2 : 0;   // full slices of two groups before the last
+    const int ngl = ng - 2 * nz;                // groups of the last slice (0, 1 or 2)
+    if (nz > 0)
+        hipLaunchKernelGGL((k_basis_mul<2, 0>), dim3(a.ntiles, nf, nz), dim3(256), 0, s, F, a, Y, X, k, t, 0);
+#define TK_BM_CASE(G_, L_)                                                                             \
+    if (ngl == G_ && tl == L_)                                                                        \
+        hipLaunchKernelGGL((k_basis_mul<G_, L_>), dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t, nz);
+    TK_BM_CASE(0, 1) TK_BM_CASE(0, 2) TK_BM_CASE(0, 3) TK_BM_CASE(0, 4)
+    TK_BM_CASE(1, 0) TK_BM_CASE(1, 1) TK_BM_CASE(1, 2) TK_BM_CASE(1, 3) TK_BM_CASE(1, 4)
+    TK_BM_CASE(2, 0) TK_BM_CASE(2, 1) TK_BM_CASE(2, 2) TK_BM_CASE(2, 3) TK_BM_CASE(2, 4)
+#undef TK_BM_CASE
 }
 #ifndef TK_GRAM_BLOCKS
 #define TK_GRAM_BLOCKS 512    // k_gram blocks (2 per CU; A/B in profiles/r03/gram_ab.txt): a function of n only

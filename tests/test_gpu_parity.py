@@ -423,8 +423,11 @@ def test_tensorkrylov_arnoldi_vs_oracle(ctx):
 
 
 def test_basis_mul_mfma(ctx):
+    """k_basis_mul against V @ Y for every column split (16-column MFMA groups, a VALU tail of
+    t mod 16 <= 4 columns, slices of 32) and k split (8-column chunks, a last chunk of <= 4
+    columns on one MFMA, a padded chunk of 5..7, 64-deep LDS chunks)."""
     tk = _tk()
-    n, K = 3000, 40
+    n, K = 3000, 66
     csc = tk.assemble_matrix(n, "Laplace")
     bs = _rhs(n, 3, 5, distinct=True)
     A = tk.DeviceMatrix(ctx, csc)
@@ -433,7 +436,8 @@ def test_basis_mul_mfma(ctx):
     for j in range(K):
         dev.step(j, False)
     rng = np.random.default_rng(0)
-    for k, t in [(40, 17), (23, 3), (41, 70), (1, 1)]:
+    for k, t in [(40, 17), (23, 3), (41, 70), (1, 1), (50, 17), (7, 20), (33, 36), (49, 52), (64, 32),
+                 (3, 2), (45, 21), (66, 4), (13, 16), (58, 5), (26, 48)]:
         Ys = [rng.standard_normal((k, t)) for _ in range(3)]
         X = dev.basis_mul(k, Ys)
         for f in range(3):

@@ -2,7 +2,7 @@
 """Host-only timing of the native iteration evaluation (tk_solver_evaluate: compressed solve
 + residual + orthogonality) at the C2 shape d = 8, K = 50 on this machine's CPU, with records
 from the CPU stand-in device (n = 200: the k-sized work does not depend on n).
-usage: python tools/host_eval_bench.py [tol]"""
+usage: python tools/host_eval_bench.py [tol] [C2|C4]"""
 import os
 import sys
 import time
@@ -15,15 +15,17 @@ import tkamd  # noqa: E402
 import _fake_device as FD  # noqa: E402
 
 tol = float(sys.argv[1]) if len(sys.argv) > 1 else 1e-9
-d, n, K = 8, 200, 50
-csc = tkamd.assemble_matrix(n, "Laplace")
+cfg = sys.argv[2] if len(sys.argv) > 2 else "C2"
+d, n, K = (8, 200, 50) if cfg == "C2" else (10, 200, 50)
+cls, inst = ("Laplace", "SymInstance") if cfg == "C2" else ("ConvDiff", "NonSymInstance")
+csc = tkamd.assemble_matrix(n, cls)
 b = [np.random.default_rng(1000 + s).random(n) for s in range(d)]
 b = [x / np.linalg.norm(x) for x in b]
-A = tkamd.KroneckerMatrix("SymInstance", [csc] * d, "Laplace")
+A = tkamd.KroneckerMatrix(inst, [csc] * d, cls)
 td = tkamd.TensorArnoldi(A, K, backend=FD.backend)
 td.orthonormalize_first(b)
 T = tkamd.compressed.IterationTables(A, K, tol, d)
-sv = tkamd.compressed.NativeSolver(td.method, d, K, True, 1.0, T)
+sv = tkamd.compressed.NativeSolver(td.method, d, K, inst == "SymInstance", 1.0, T)
 f = FD.FakeDecomposition(td, b)
 sv.apply(-1, f.init())
 for j in range(K):
