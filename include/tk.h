@@ -222,6 +222,14 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
  * orthogonality_data of factor 1 (src/tensor_krylov_method.jl:103): orthogonality_data[k] =
  * norm(G[0..k, 0..k] - I) for every k from one G, instead of a Gram row in every step. */
 tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G);
+/* The same Gram launched AHEAD, asynchronously, over the longest prefix of columns that are
+ * already written (no flush, so no record exchange: safe on one rank of many), when this rank
+ * holds global factor 0 of a deferred-Gram handle (else nothing happens; *k_out = 0).
+ * tk_solver_run calls it as soon as the last step of the loop is issued, so the SYRK runs right
+ * behind the steps while the host evaluates the last iterations; a later tk_decomp_gram(dc, 0,
+ * k, G) with k <= *k_out reads the leading k x k block of that result instead of launching
+ * (columns 0..k-1 never change until the next tk_decomp_init, which drops it). */
+tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out);
 /* 1 when global factor 0's Gram rows are NOT carried in the step records (its record's
  * "tracked" field is 0) and orthogonality_data comes from tk_decomp_gram at the end: the
  * default for TK_ARNOLDI / TK_LANCZOS with kmax < 64 (the one-sweep Lanczos step reads no
@@ -233,8 +241,10 @@ int tk_decomp_gram_deferred(tk_decomp* dc);
 
 /* Launch streams of the one-sweep Arnoldi step: 2 when the local factors step as two groups,
  * each in its own launches on its own stream of the context (one group's launch drain and
- * reduce overlap the other's sweep), else 1.  Groups apply on a single rank (no records
- * exchange) with nf >= 2; TKHIP_FACTOR_GROUPS=1 at create keeps one stream.  Results are
+ * reduce overlap the other's sweep), else 1.  Groups apply with nf >= 2 local factors, on a
+ * single rank or under a records exchange whose steps signal through the signal word (both
+ * groups' bookkeeping blocks count into it; slot guards are waited for on both streams);
+ * TKHIP_FACTOR_GROUPS=1 at create keeps one stream.  Results are
  * bitwise those of one stream (every kernel is per factor). */
 int tk_decomp_factor_groups(tk_decomp* dc);
 

@@ -697,6 +697,10 @@ struct tk_decomp {
     bool forked = false;
     hipEvent_t fev_fork = nullptr, fev_join = nullptr;
     bool gram_inflight = false;
+    // the Gram launched ahead by tk_decomp_gram_ahead (0: none for this sequence): its column
+    // count and the sequence number its host mirror publishes
+    int ahead_k = 0;
+    unsigned long long ahead_want = 0;
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
@@ -1372,6 +1376,7 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     dc->jnext = 0;
     dc->pending = false;
     dc->last_j = -1;
+    dc->ahead_k = 0;   // (a Gram launched ahead belongs to the previous sequence)
     // a new sequence: slots of the previous one that never went out are dropped (on every rank)
     dc->xs.reset();
     dc->xcnt[0] = dc->xcount;
@@ -1841,6 +1846,24 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     TK_API_END
 }
 
+// wait (host spin on the mapped sequence word) for the Gram whose mirror publishes `want`
+static tk_status gram_wait(tk_decomp* dc, hipStream_t s, unsigned long long want) {
+    tk_ctx* c = dc->ctx;
+    long spins = 0;
+    Deadline dl;
+    while (__atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want) {
+        if (++spins % 4096 == 0) {
+            hipError_t e = hipStreamQuery(s);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want)
+                return fail(TK_ERR_STATE, "tk_decomp_gram: the result never arrived");
+            if (c->comm && dl.elapsed() > dl.lim)
+                return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
+        }
+    }
+    return TK_OK;
+}
+
 tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     CHECKARG(dc, "NULL argument");
     CHECKARG(f >= 0 && f < dc->nf, "factor out of range");
@@ -1849,6 +1872,18 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     HIPCHK(hipSetDevice(c->device));
     GJOIN(dc);
     if (dc->failed) return fail(TK_ERR_STATE, "an earlier step of this decomposition failed");
+    if (f == 0 && dc->ahead_k >= k && dc->gram_host) {
+        // launched ahead (tk_decomp_gram_ahead) over these columns: read its leading block
+        if (!G) return TK_OK;
+        tk_status st = gram_wait(dc, c->stream, dc->ahead_want);
+        if (st) return st;
+        std::vector<double> full((size_t)dc->ahead_k * dc->ahead_k);
+        gram_unpack(dc->ahead_k, dc->gram_host, full.data());
+        for (int j = 0; j < k; ++j)
+            for (int i = 0; i < k; ++i) G[(size_t)j * k + i] = full[(size_t)j * dc->ahead_k + i];
+        return TK_OK;
+    }
+    dc->ahead_k = 0;   // (this launch's mirror replaces the one launched ahead)
     // every column the product reads must be in V: flush a pending (or column-buffered) one
     const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
@@ -1896,19 +1931,8 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         const unsigned long long want = ++dc->gram_seq;
         launch_mirror_records(res, dc->gram_host, nv, dc->gram_done, 1, want, s);
         LAUNCHCHK("gram mirror");
-        long spins = 0;
-        Deadline dl;
-        while (__atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want) {
-            if (++spins % 4096 == 0) {
-                hipError_t e = hipStreamQuery(s);
-                if (e != hipSuccess && e != hipErrorNotReady)
-                    return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
-                if (e == hipSuccess && __atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want)
-                    return fail(TK_ERR_STATE, "tk_decomp_gram: the result never arrived");
-                if (c->comm && dl.elapsed() > dl.lim)
-                    return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
-            }
-        }
+        tk_status st = gram_wait(dc, s, want);
+        if (st) return st;
     } else {
         vbuf.resize(nv);
         HIPCHK(hipMemcpyAsync(vbuf.data(), res, nv * sizeof(double), hipMemcpyDeviceToHost, s));
@@ -1916,6 +1940,46 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         v = vbuf.data();
     }
     gram_unpack(k, v, G);
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out) { TK_API_BEGIN
+    CHECKARG(dc && k_out, "NULL argument");
+    *k_out = 0;
+    tk_ctx* c = dc->ctx;
+    // only the rank holding global factor 0 (not a replica) of a deferred-Gram handle, with
+    // the host mirror available, and never twice per sequence
+    static const bool off = [] {   // TKHIP_GRAM_AHEAD=0: the Gram waits for the caller (A/B, tests)
+        const char* e = getenv("TKHIP_GRAM_AHEAD");
+        return e && e[0] == '0';
+    }();
+    if (off || !dc->gram_deferred || dc->foff != 0 || dc->nf <= 0 || dc->zrec || !dc->gram_host || dc->failed ||
+        !dc->inited || dc->ahead_k > 0)
+        return TK_OK;
+    // written columns only (no flush: it would start record exchanges on one rank)
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+                      dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
+    int k = dc->pending ? dc->last_j + (in_e ? 0 : 1) : dc->jnext + 1;
+    k = std::min(std::min(k, 64), dc->kmax + 1);
+    if (k < 2) return TK_OK;
+    HIPCHK(hipSetDevice(c->device));
+    GJOIN(dc);
+    if (!dc->gram_scr) HIPCHK(hipMalloc((void**)&dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double)));
+    hipStream_t s = c->stream;
+    {
+        Timer tm(c, TCLS_GRAM, 1, s);
+        KArgs a = base_args(dc, 0, 0);
+        launch_gram(dc->df, 0, a, k, dc->gram_scr, s);
+    }
+    LAUNCHCHK("gram ahead");
+    const unsigned long long want = ++dc->gram_seq;
+    launch_mirror_records(dc->gram_scr + gram_result_offset(dc->ntiles, k), dc->gram_host, gram_values(k),
+                          dc->gram_done, 1, want, s);
+    LAUNCHCHK("gram ahead mirror");
+    dc->ahead_k = k;
+    dc->ahead_want = want;
+    *k_out = k;
     return TK_OK;
     TK_API_END
 }

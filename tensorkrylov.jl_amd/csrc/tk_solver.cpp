@@ -322,7 +322,18 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         }
         return TK_OK;
     };
+    // the deferred orthogonality Gram of factor 1 goes to the device right behind the last
+    // step (tk_decomp_gram_ahead: no-op on ranks without it), overlapping the host's evaluation
+    // of the last iterations; the caller's tk_decomp_gram then only reads it
+    bool gram_ahead = false;
+    auto ahead = [&]() -> tk_status {
+        if (gram_ahead || next_issue <= kmax) return TK_OK;
+        gram_ahead = true;
+        int kg = 0;
+        return tk_decomp_gram_ahead(dc, &kg);
+    };
     tk_status st = issue_upto(kfirst + depth - 1);
+    if (!st) st = ahead();
     if (st) return st;
 
     std::vector<Worker> workers(P);
@@ -404,6 +415,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             err = tk_decomp_records(dc, k_dispatch, k_dispatch + 1, rec.data());
             lap(t_rec);
             if (!err) err = issue_upto(k_dispatch + depth);
+            if (!err) err = ahead();
             lap(t_issue);
             if (err) break;
             apply_record(sv, k_dispatch - 1, rec.data());

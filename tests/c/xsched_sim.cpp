@@ -124,6 +124,12 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) {
     return TK_OK;
 }
 
+tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out) {   // (no collective: nothing to log)
+    (void)dc;
+    *k_out = 0;
+    return TK_OK;
+}
+
 tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
     if (s1 > s0) need_slots(dc, std::min(s1 - 1, dc->jnext));
     memset(out, 0, sizeof(double) * (s1 - s0) * dc->d * dc->m);
