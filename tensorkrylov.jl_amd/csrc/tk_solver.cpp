@@ -42,6 +42,7 @@ tk_status tk_fail_internal(int code, const char* msg);   // tk_abi.cpp: tk_last_
 namespace {
 
 struct IterResult {
+    double t0 = -1.0, t1 = -1.0;   // evaluation start / end, steady_clock seconds (TKHIP_SOLVER_TRACE)
     int k = 0;
     int status = TK_OK;           // TK_OK, TK_BREAKDOWN or TK_ERR_STATE (eigen/expm failure)
     double r_comp = 0.0, r_norm = 0.0, rel = 0.0, orth = 0.0;
@@ -349,7 +350,10 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
                     k = wk.job;
                 }
                 if (k < 0) return;
+                const double tb = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
                 evaluate(sv, k, wk.res, wk.ws);
+                wk.res.t0 = tb;
+                wk.res.t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
                 {
                     std::lock_guard<std::mutex> lk(wk.mu);
                     wk.job = 0;
@@ -408,6 +412,13 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         tp = now;
     };
     const auto t_begin = clk::now();
+    // TKHIP_SOLVER_TRACE=path: per iteration, microseconds from the loop start at which its
+    // record was in hand, its evaluation started and ended (worker clock), and it was consumed
+    const char* etr = getenv("TKHIP_SOLVER_TRACE");
+    std::vector<double> tr_rec(kmax + 2, -1.0), tr_cons(kmax + 2, -1.0);
+    auto since = [&](clk::time_point p) { return std::chrono::duration<double, std::micro>(p - t_begin).count(); };
+    for (auto& wk : workers) wk.res.t0 = wk.res.t1 = -1.0;
+    std::vector<double> tr_e0(kmax + 2, -1.0), tr_e1(kmax + 2, -1.0);
     for (int k = kfirst; k <= klast; ++k) {
         // keep P evaluations in flight: records of step k_dispatch-1, applied in order
         while (k_dispatch <= klast && k_dispatch < k + P) {
@@ -419,6 +430,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             lap(t_issue);
             if (err) break;
             apply_record(sv, k_dispatch - 1, rec.data());
+            if (etr) tr_rec[k_dispatch] = since(clk::now());
             submit((k_dispatch - kfirst) % P, k_dispatch);
             ++k_dispatch;
             lap(t_apply);
@@ -428,6 +440,11 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         wait_done((k - kfirst) % P, k);
         lap(t_wait);
         IterResult& r = wk.res;
+        if (etr) {
+            tr_cons[k] = since(clk::now());
+            tr_e0[k] = r.t0 >= 0 ? std::chrono::duration<double, std::micro>(std::chrono::duration<double>(r.t0)).count() : -1;
+            tr_e1[k] = r.t1 >= 0 ? std::chrono::duration<double, std::micro>(std::chrono::duration<double>(r.t1)).count() : -1;
+        }
         if (r.status == TK_ERR_STATE) {
             err = tk_fail_internal(TK_ERR_STATE, "compressed solve failed (eigen / expm)");
             break;
@@ -450,6 +467,16 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         if (k == klast) std::swap(sv->last, r);
     }
     stop_workers();
+    if (etr) {
+        if (FILE* f = fopen(etr, "w")) {
+            fprintf(f, "k,record_us,eval_start_us,eval_end_us,consumed_us\n");
+            const double base = std::chrono::duration<double>(t_begin.time_since_epoch()).count();
+            for (int k = kfirst; k <= *k_end; ++k)
+                fprintf(f, "%d,%.1f,%.1f,%.1f,%.1f\n", k, tr_rec[k], tr_e0[k] >= 0 ? tr_e0[k] - 1e6 * base : -1.0,
+                        tr_e1[k] >= 0 ? tr_e1[k] - 1e6 * base : -1.0, tr_cons[k]);
+            fclose(f);
+        }
+    }
     if (stats)
         fprintf(stderr, "tk_solver_run: %d iterations, %d threads, %.1f us total: records %.1f, issue %.1f, "
                         "apply+submit %.1f, wait results %.1f (us per iteration)\n",
