@@ -1017,8 +1017,13 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         // slot then waits for the count both groups' bookkeeping blocks add (an event marker
         // would sit in one group's stream only), and every slot guard is waited for on both
         // group streams (slot_guard)
+        // One-sweep Lanczos groups its Gram-free steps (k_lan_1w + k_red_lan) the same way:
+        // each launch's bookkeeping blocks mirror and signal their own group's factors (host
+        // words offset by the group's first factor), k_red_lan writes only device records
         const char* eg = getenv("TKHIP_FACTOR_GROUPS");
-        if ((dc->recv == dc->rec || dc->xflag) && method == TK_ARNOLDI && dc->onesweep && nf >= 2 && !(eg && eg[0] == '1') &&
+        const bool lan_ok = method == TK_LANCZOS && !dc->any_gram;
+        if ((dc->recv == dc->rec || dc->xflag) && (method == TK_ARNOLDI || lan_ok) && dc->onesweep && nf >= 2 &&
+            !(eg && eg[0] == '1') &&
             hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess &&
             hipEventCreateWithFlags(&dc->fev_join, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess)
             dc->g1 = nf / 2;
@@ -1446,7 +1451,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         ax.seq = ++dc->seq;
     }
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
-    const bool grouped = dc->g1 > 0 && dc->method == TK_ARNOLDI && dc->onesweep && j <= ARN_D1_JMAX;
+    const bool grouped = dc->g1 > 0 && (dc->method == TK_ARNOLDI || (dc->method == TK_LANCZOS && !dc->any_gram)) &&
+                         dc->onesweep && j <= ARN_D1_JMAX;
     if (!grouped) GJOIN(dc);
     if ((dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && j > ARN_D1_JMAX && dc->pending &&
         dc->last_j <= ARN_D1_JMAX) {
@@ -1547,8 +1553,32 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             an.xflag = nullptr;
             an.hdone = nullptr;
             an.hrec = nullptr;
-            RUN(TCLS_PASS1, 2, launch_lan_1w(dc->df, nf, a, b, dc->nwl, s), "lan_1w");
-            RUN(TCLS_RED, 2, launch_red_lan(dc->df, nf, an, s), "red_lan");
+            if (grouped) {
+                // each factor group's window launch + reduce on its own stream (as the Arnoldi
+                // groups); the leading blocks of a group's launch mirror and signal the
+                // previous step's records of that group's factors: host words offset by g0
+                tk_status stf = fork_groups(dc);
+                if (stf) return stf;
+                for (int g = 0; g < 2; ++g) {
+                    const int g0 = g ? dc->g1 : 0, ng = g ? nf - dc->g1 : dc->g1;
+                    hipStream_t sg = g ? c->fstream : s;
+                    KArgs bg = b;
+                    if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
+                    {
+                        Timer tm_(c, TCLS_PASS1, 2, sg);
+                        launch_lan_1w(dc->df + g0, ng, a, bg, dc->nwl, sg);
+                    }
+                    LAUNCHCHK("lan_1w");
+                    {
+                        Timer tm_(c, TCLS_RED, 2, sg);
+                        launch_red_lan(dc->df + g0, ng, an, sg);
+                    }
+                    LAUNCHCHK("red_lan");
+                }
+            } else {
+                RUN(TCLS_PASS1, 2, launch_lan_1w(dc->df, nf, a, b, dc->nwl, s), "lan_1w");
+                RUN(TCLS_RED, 2, launch_red_lan(dc->df, nf, an, s), "red_lan");
+            }
             dc->bk_j = j;
             dc->bk_args = ax;
             dc->bk_kind = 1;

@@ -207,3 +207,71 @@ def test_c4_convdiff_2p17_all_factors_and_vy(ctx):
     """C4 (configs[4]): d = 10, n_s = 2^17 ConvDiff (nonsymmetric, 4 diagonals), K = 50, one-
     sweep Arnoldi, every factor; V*Y at the solver's exp-sum rank t = 3 for each factor."""
     _check_arnoldi(ctx, "ConvDiff", 1 << 17, 10, 50, check=range(10), expect_sweeps=1, vy_t=3)
+
+
+def test_c2_laplace_2p20_lanczos_all_8_factors(ctx):
+    """C2 with TensorLanczos (the one-sweep TTR step the bench line 'c2_TensorLanczos' times,
+    k_lan_1w + k_red_lan with the deferred Gram): d = 8, n_s = 2^20 Laplace, K = 50, swept
+    exactly as bench.py does, every factor checked against the C oracle's TTR
+    (src/orthogonal_bases.jl:39-67): alpha, beta and V while the oracle basis is orthonormal
+    (1e-12), one oracle step from the device's state at every step (shadowing, rounding only),
+    and the three-term relation on the device basis."""
+    from oracle import tk_ref
+    tk = _tk()
+    n, K, d = 1 << 20, 50, 8
+    csc = tk.assemble_matrix(n, "Laplace")
+    bs = _bench_rhs(n, d)
+    A = tk.DeviceMatrix(ctx, csc)
+    dev = tk.DeviceDecomposition(ctx, tk._lib.TK_LANCZOS, d, 0, [A] * d, bs, K)
+    assert dev.arnoldi_sweeps == 1 and dev.gram_deferred
+    dev.init(False)
+    dev.sweep(0, K)
+    dev.flush(False)
+    recs = dev.records(0, K + 1)
+    S = _spm(csc)
+    for f in range(d):
+        al = np.array([recs[j + 1][f, j] for j in range(K)])
+        be = np.array([recs[j + 1][f, j + 1] for j in range(K)])
+        V = dev.basis(f, 0, K + 1)
+        ref = tk_ref.RefFactor(csc, bs[f], K)
+        j_orth = K
+        for j in range(K):
+            ref.lanczos_step(j)
+            if j % 5 == 4 or j == K - 1:
+                G = ref.V[:, :j + 2].T @ ref.V[:, :j + 2]
+                if np.linalg.norm(G - np.eye(j + 2)) > 1e-10:
+                    j_orth = j - 4
+                    break
+        scale = max(np.abs(np.diag(ref.H)[:K]).max(), 1.0)
+        ea = np.abs(al[:j_orth] - np.diag(ref.H)[:j_orth]).max() / scale
+        eb = np.abs(be[:j_orth] - np.diag(ref.H, -1)[:j_orth]).max() / scale
+        eV = np.abs(V[:, :j_orth + 1] - ref.V[:, :j_orth + 1]).max()
+        del ref
+        sh = tk_ref.RefFactor(csc, bs[f], K)
+        sa = sb = sv = 0.0
+        for j in range(K):
+            if j > 0:
+                sh.V[:, j - 1] = V[:, j - 1]
+                sh.beta = be[j - 1]
+            sh.V[:, j] = V[:, j]
+            a_, b_ = sh.lanczos_step(j)
+            sa = max(sa, abs(a_ - al[j]) / scale)
+            sb = max(sb, abs(b_ - be[j]) / scale)
+            sv = max(sv, np.abs(sh.V[:, j + 1] - V[:, j + 1]).max())
+        del sh
+        AVl = S @ V
+        er = 0.0
+        for j in range(1, K):
+            r = AVl[:, j] - be[j - 1] * V[:, j - 1] - al[j] * V[:, j] - be[j] * V[:, j + 1]
+            er = max(er, np.abs(r).max() / scale)
+        print("C2 Lanczos factor %d: orthonormal through step %d: alpha %.2e beta %.2e V %.2e; "
+              "shadowing: alpha %.2e beta %.2e v %.2e; ttr %.2e" % (f, j_orth, ea, eb, eV, sa, sb, sv, er))
+        assert j_orth >= 30                   # Laplace at 2^20 stays orthonormal for most of K
+        assert ea <= 1e-12 and eb <= 1e-12    # alpha, beta: 1e-12 relative (trajectory)
+        assert eV <= 1e-12                    # V: 1e-12 absolute (trajectory)
+        assert sa <= 1e-13 and sb <= 1e-13    # one step from the same state: rounding only
+        assert sv <= 1e-13
+        assert er <= 1e-11                    # three-term relation
+        del V, AVl
+    dev.close()
+    A.close()

@@ -102,3 +102,45 @@ def test_factor_groups_under_records_exchange(ctx, grp, monkeypatch):
         assert np.array_equal(a, b)
     for a, b in zip(local[3], xch[3]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("d", [2, 5])
+def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
+    """One-sweep TensorLanczos without Gram rows (k_lan_1w + k_red_lan, the deferred Gram)
+    steps its factors as two groups on two streams: records (taken one step at a time and as a
+    sweep), the basis, the flushed column and V*Y bitwise those of one stream."""
+    import tkamd as tk
+    monkeypatch.delenv("TKHIP_GRAM", raising=False)
+    n, K, t = 3000, 40, 5
+    rng = np.random.default_rng(78)
+    mat = tk.assemble_matrix(n, "Laplace")
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    Ys = [rng.standard_normal((K, t)) for _ in range(d)]
+    out = {}
+    for G in ("1", "2"):
+        monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
+        A = tk.DeviceMatrix(ctx, mat)
+        dev = tk.DeviceDecomposition(ctx, tk._lib.TK_LANCZOS, d, 0, [A] * d, bs, K)
+        assert dev.arnoldi_sweeps == 1 and dev.gram_deferred
+        assert dev.factor_groups == int(G)
+        r0 = dev.init()
+        recs = [dev.step(j) for j in range(9)]
+        for j in range(9, 17):
+            dev.step_async(j)
+        recs.append(dev.records(10, 17))
+        dev.sweep(17, K)
+        recs.append(dev.records(0, K + 1))
+        V = [dev.basis(f, 0, K) for f in range(d)]
+        X = dev.basis_mul(K, Ys)
+        recs.append(dev.records(K + 1, K + 2))
+        out[G] = (r0, recs, V, X)
+        dev.close()
+        A.close()
+    (a0, ar, aV, aX), (b0, br, bV, bX) = out["1"], out["2"]
+    assert np.array_equal(a0, b0)
+    for x, y in zip(ar, br):
+        assert np.array_equal(x, y)
+    for x, y in zip(aV, bV):
+        assert np.array_equal(x, y)
+    for x, y in zip(aX, bX):
+        assert np.array_equal(x, y)
