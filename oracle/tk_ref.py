@@ -184,7 +184,12 @@ def baseline_all_cores(csc, n, d, K, seconds=10.0, threads=None):
         if time.perf_counter() - t_start >= seconds or s >= 4 * d:
             break
     per_iter = d * float(np.mean(sweeps)) / K
+    omp = os.environ.get("OMP_NUM_THREADS")
     return {"value": round(1.0 / per_iter, 4), "unit": "iterations/s", "cores": int(threads), "kind": "port",
             "sample": "oracle/tk_ref.c MGS2 Arnoldi, rows over %d OpenMP threads, full K=%d sweeps of %d "
                       "factor(s) of the workload (n=%d; d=%d), %.1f s, mean sweep x d"
-                      % (threads, K, len(sweeps), n, d, float(np.sum(sweeps)))}
+                      % (threads, K, len(sweeps), n, d, float(np.sum(sweeps))),
+            # the thread count is the process's CPU share, not the machine: the GPU box sets
+            # OMP_NUM_THREADS (16 per GPU) although the host shows all of its CPUs
+            "cores_cap": ("OMP_NUM_THREADS=%s: the CPU share given to this job; the host has %s CPUs "
+                          "(not all used)" % (omp, os.cpu_count())) if omp else None}

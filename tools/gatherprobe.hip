@@ -6,6 +6,10 @@
 //   matrix   the index / value stream alone (no gathers): the matrix-read floor
 //   seqgath  kernel's loads with every gathered row replaced by the thread's own row
 //            (sequential 64-B rows): what the same bytes cost without the random pattern
+//   split40  the 40-B entry as 32 B (factors 0-3, rows at a 32-B pitch) + 8 B (factor 4, its
+//            own array): lanes 0, 1 of a quad gather 16 B each of the 32-B piece, lane 2 the 8 B
+//   pack40   the 40-B entry packed (rows at a 40-B pitch, no padding): lanes 0, 1 16 B each
+//            (8-B aligned), lane 2 the last 8 B -- a row may straddle two 64-B segments
 //   gath64   one 64-B gather per nonzero, no index/value loads (indices precomputed per
 //            thread in registers is impossible; instead col = hash(row, q)): random-gather floor
 // Reports microseconds (mean of 20) and the algorithmic bytes rate of the SpMV
@@ -131,6 +135,57 @@ __global__ __launch_bounds__(TPB) void k_coop4(Sell A, const double* __restrict_
     }
 }
 
+// the 40-byte entry: SPLIT 1 -> U4 (32-B rows) + U1 (8-B rows); SPLIT 0 -> one 40-B-pitch array
+template <int SPLIT>
+__global__ __launch_bounds__(TPB) void k_e40(Sell A, const double* __restrict__ U4, const double* __restrict__ U1,
+                                             double* __restrict__ AU, int64_t ld) {
+    constexpr int SG = 4;
+    const int p = threadIdx.x & 3;
+    const int64_t r = (int64_t)blockIdx.x * (TPB / 4) + (threadIdx.x >> 2);
+    if (r >= ld) return;
+    double s0 = 0.0, s1 = 0.0;
+    if (r < A.n && p < 3) {
+        const int64_t t = r >> 8;
+        const int l = (int)(r & 255);
+        const int64_t base = A.sptr[t];
+        const int w = A.swidth[t];
+        const int len = A.rowlen[r];
+        for (int q0 = 0; q0 < w; q0 += SG) {
+            int64_t cc[SG];
+            double vv[SG];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                const int64_t e = base + (int64_t)(q0 + g) * TPB + l;
+                const bool in = q0 + g < len;
+                cc[g] = in ? (int64_t)A.scol[e] : -1;
+                vv[g] = in ? A.sval[e] : 0.0;
+            }
+            d2 x[SG];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                if (cc[g] < 0) {
+                    x[g] = (d2){0.0, 0.0};
+                } else if (SPLIT) {
+                    x[g] = p < 2 ? ((const d2*)(U4 + cc[g] * 4))[p] : (d2){U1[cc[g]], 0.0};
+                } else {
+                    const double* row = U4 + cc[g] * 5;
+                    x[g] = p < 2 ? *(const d2*)__builtin_assume_aligned(row + 2 * p, 8) : (d2){row[4], 0.0};
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < SG; ++g)
+                if (cc[g] >= 0) {
+                    s0 = add_rn(s0, mul_rn(vv[g], x[g].x));
+                    s1 = add_rn(s1, mul_rn(vv[g], x[g].y));
+                }
+        }
+    }
+    if (p < 3) {
+        AU[(int64_t)(2 * p) * ld + r] = s0;
+        if (2 * p + 1 < NF) AU[(int64_t)(2 * p + 1) * ld + r] = s1;
+    }
+}
+
 // one 64-B (4 x 16 B) random gather per nonzero slot, columns from a hash: no matrix stream
 __global__ __launch_bounds__(TPB) void k_gath64(int64_t n, int w, const double* __restrict__ Ui, double* __restrict__ AU, int64_t ld) {
     const int p = threadIdx.x & 3;
@@ -214,6 +269,27 @@ int main(int argc, char** argv) {
     rep("kernel", timeit([&] { k_thread<0><<<nb, TPB>>>(A, Ui, AU, ld); }, reps));
     rep("coop4", timeit([&] { k_coop4<4><<<(int)(ld / 64), TPB>>>(A, Ui, AU, ld); }, reps));
     rep("coop4sg8", timeit([&] { k_coop4<8><<<(int)(ld / 64), TPB>>>(A, Ui, AU, ld); }, reps));
+    {
+        std::vector<double> u4(ld * 4), u1(ld), u5(ld * 5);
+        for (int64_t i = 0; i < ld; ++i) {
+            for (int q = 0; q < 4; ++q) u4[i * 4 + q] = u[i * NP + q];
+            u1[i] = u[i * NP + 4];
+            for (int q = 0; q < 5; ++q) u5[i * 5 + q] = u[i * NP + q];
+        }
+        double* U4 = up(u4);
+        double* U1 = up(u1);
+        double* U5 = up(u5);
+        const double g40 = 40.0 * nnz;
+        auto rep40 = [&](const char* name, float ms) {
+            printf("%-10s %8.1f us  alg %6.2f TB/s  (40-B entries %6.2f TB/s)\n", name, ms * 1e3,
+                   alg / (ms * 1e-3) / 1e12, g40 / (ms * 1e-3) / 1e12);
+        };
+        rep40("split40", timeit([&] { k_e40<1><<<(int)(ld / 64), TPB>>>(A, U4, U1, AU, ld); }, reps));
+        rep40("pack40", timeit([&] { k_e40<0><<<(int)(ld / 64), TPB>>>(A, U5, nullptr, AU, ld); }, reps));
+        CK(hipFree(U4));
+        CK(hipFree(U1));
+        CK(hipFree(U5));
+    }
     rep("matrix", timeit([&] { k_thread<1><<<nb, TPB>>>(A, Ui, AU, ld); }, reps));
     rep("seqgath", timeit([&] { k_thread<2><<<nb, TPB>>>(A, Ui, AU, ld); }, reps));
     const int wavg = (int)((nnz + n - 1) / n);
