@@ -7,3 +7,5 @@ python3 tools/c3_sell_dump.py /tmp/c3_sell.bin > gpurun_out/c3_dump.log 2>&1 || 
 timeout -k 10 120 tools/_build/gatherprobe /tmp/c3_sell.bin > gpurun_out/c3_gatherprobe.txt 2>&1 || { echo "probe failed"; cat gpurun_out/c3_gatherprobe.txt; exit 1; }
 cat gpurun_out/c3_gatherprobe.txt
 bash tools/gpu/r3_c3pmc.sh
+timeout -k 10 120 tools/_build/syncprobe > gpurun_out/syncprobe.txt 2>&1 || { echo "syncprobe failed"; cat gpurun_out/syncprobe.txt; exit 1; }
+cat gpurun_out/syncprobe.txt
