@@ -906,6 +906,9 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_RS64
 #define TK_D1_RS64 1
 #endif
+#ifndef TK_D1_XMAP
+#define TK_D1_XMAP 0
+#endif
 // Register rows of at least TK_D1_LCMIN columns keep their lowest TK_D1_LC columns in LDS,
 // loaded there directly (buffer_load ... lds, no VGPR destination) and read back as each use
 // comes: the register budget of a row TK_D1_LC columns narrower -- one wave per SIMD more,
@@ -1012,7 +1015,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         return;
     }
     const int bx = (int)blockIdx.x - x0;
-    const int slot = (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
+    // (TK_D1_XMAP=1, A/B builds only: windows interleaved over the XCDs instead)
+    const int slot = TK_D1_XMAP ? bx : (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
     if (slot >= d.nwin) return;
 #else
     if ((int)blockIdx.x >= d.npd) return;

@@ -12,6 +12,6 @@ if [ "$rev" != "-" ]; then
     mkdir -p $src/$(dirname $f); git -C $R show $rev:$f > $src/$f 2>/dev/null || rm -f $src/$f
   done
 fi
-hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Wno-unused-value -Wno-unused-result "$@" \
+hipcc --offload-arch=gfx950 -O3 -fPIC -shared -std=c++17 -Xarch_host -mavx2 -Xarch_host -mfma -Wno-unused-value -Wno-unused-result "$@" \
   -I $src/include $src/tensorkrylov.jl_amd/csrc/tk_kernels.hip $src/tensorkrylov.jl_amd/csrc/tk_abi.cpp $( [ -f $src/tensorkrylov.jl_amd/csrc/tk_host.cpp ] && echo $src/tensorkrylov.jl_amd/csrc/tk_host.cpp ) $( [ -f $src/tensorkrylov.jl_amd/csrc/tk_solver.cpp ] && echo $src/tensorkrylov.jl_amd/csrc/tk_solver.cpp ) -pthread -lrccl \
   -o $R/tools/_build/libtkhip_$name.so
