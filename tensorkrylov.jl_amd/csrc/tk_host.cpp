@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/tk.h"
@@ -272,8 +273,17 @@ void ExpmPowers::reset(int n_, const double* A_) {
         for (int i = 0; i < n; ++i) s += fabs(A[(size_t)j * n + i]);
         norm1 = std::max(norm1, s);
     }
-    const size_t nn = (size_t)n * n;
-    for (Vec* v : {&U, &V, &T, &Num, &Den}) v->resize(nn);
+}
+
+static const double kTheta[] = {1.495585217958292e-2, 2.539398330063230e-1, 9.504178996162932e-1,
+                                2.097847961257068e0, 5.371920351148152e0};
+
+int ExpmPowers::needs(double c) const {
+    const double nrm = fabs(c) * norm1;
+    static const int top[] = {2, 4, 6, 8};   // Pade degree 3/5/7/9 reads powers up to m - 1
+    for (int q = 0; q < 4; ++q)
+        if (nrm <= kTheta[q]) return top[q];
+    return 6;                                // degree 13: A^2, A^4, A^6
 }
 
 const double* ExpmPowers::pw(int k) {
@@ -285,14 +295,13 @@ const double* ExpmPowers::pw(int k) {
     return k == 2 ? P2.data() : k == 4 ? P4.data() : k == 6 ? P6.data() : P8.data();
 }
 
-static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
+static bool expm_scaled(ExpmPowers& pw, ExpmScratch& xs, double c, Vec& E) {
     static const double b13[] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
                                  1187353796428800.0,  129060195264000.0,   10559470521600.0,
                                  670442572800.0,      33522128640.0,       1323241920.0,
                                  40840800.0,          960960.0,            16380.0,
                                  182.0,               1.0};
-    static const double theta[] = {1.495585217958292e-2, 2.539398330063230e-1, 9.504178996162932e-1,
-                                   2.097847961257068e0, 5.371920351148152e0};
+    const double* theta = kTheta;
     static const double bd[4][10] = {{120.0, 60.0, 12.0, 1.0},
                                      {30240.0, 15120.0, 3360.0, 420.0, 30.0, 1.0},
                                      {17297280.0, 8648640.0, 1995840.0, 277200.0, 25200.0, 1512.0, 56.0, 1.0},
@@ -302,9 +311,10 @@ static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
     const size_t nn = (size_t)n * n;
     const double* A = pw.A;
     const double norm1 = fabs(c) * pw.norm1;
-    double* U = pw.U.data();
-    double* V = pw.V.data();
-    double* T = pw.T.data();
+    for (Vec* v : {&xs.U, &xs.V, &xs.T, &xs.Num, &xs.Den}) v->resize(nn);
+    double* U = xs.U.data();
+    double* V = xs.V.data();
+    double* T = xs.T.data();
     static const int degs[] = {3, 5, 7, 9};
     int m = 13, s = 0;
     for (int q = 0; q < 4; ++q)
@@ -341,7 +351,7 @@ static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
         const double* b = b13;
         // U = As (B6 (b13 B6 + b11 B4 + b9 B2) + b7 B6 + b5 B4 + b3 B2 + b1 I),
         // V = B6 (b12 B6 + b10 B4 + b8 B2) + b6 B6 + b4 B4 + b2 B2 + b0 I   (B2k = (sc A)^2k)
-        double* W = pw.Num.data();
+        double* W = xs.Num.data();
         for (size_t i = 0; i < nn; ++i) T[i] = b[13] * s6 * B6[i] + b[11] * s4 * B4[i] + b[9] * s2 * B2[i];
         matmul(n, B6, T, W);
         for (size_t i = 0; i < nn; ++i) W[i] = s6 * W[i] + b[7] * s6 * B6[i] + b[5] * s4 * B4[i] + b[3] * s2 * B2[i];
@@ -353,8 +363,8 @@ static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
         for (size_t i = 0; i < nn; ++i) V[i] = s6 * V[i] + b[6] * s6 * B6[i] + b[4] * s4 * B4[i] + b[2] * s2 * B2[i];
         for (int i = 0; i < n; ++i) V[(size_t)i * n + i] += b[0];
     }
-    Vec& Num = pw.Num;
-    Vec& Den = pw.Den;
+    Vec& Num = xs.Num;
+    Vec& Den = xs.Den;
     for (size_t i = 0; i < nn; ++i) {
         Num[i] = V[i] + U[i];
         Den[i] = V[i] - U[i];
@@ -370,8 +380,9 @@ static bool expm_scaled(ExpmPowers& pw, double c, Vec& E) {
 
 bool expm(int n, const double* A, Vec& E) {
     ExpmPowers pw;
+    ExpmScratch xs;
     pw.reset(n, A);
-    return expm_scaled(pw, 1.0, E);
+    return expm_scaled(pw, xs, 1.0, E);
 }
 
 
@@ -528,23 +539,45 @@ bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, co
             }
         gemm_nn(k, t * d, k, Q, k, ws.M.data(), k, Y, k);
     } else {
-        // every term exp(g_j H1) from the same powers of H1 (ExpmPowers)
+        // every term exp(g_j H1) from the same powers of H1 (ExpmPowers); with ws.nthreads > 1
+        // the terms are spread over threads (the powers formed first, then read-only; each
+        // term's arithmetic is the same whichever thread runs it)
         ws.G.resize((size_t)k * k);
         for (int c = 0; c < k; ++c)
             for (int i = 0; i < k; ++i) ws.G[(size_t)c * k + i] = H1[(size_t)c * ldh + i];
         ws.pw.reset(k, ws.G.data());
-        for (int j = 0; j < t; ++j) {
+        auto term = [&](int j, ExpmScratch& xs) -> bool {
             const double g = -alpha[j] * inv;
-            if (!expm_scaled(ws.pw, g, ws.Ex)) return false;
+            if (!expm_scaled(ws.pw, xs, g, xs.Ex)) return false;
             for (int s = 0; s < d; ++s) {
                 double* y = Y + (size_t)s * k * t + (size_t)j * k;
                 for (int i = 0; i < k; ++i) y[i] = 0.0;
                 for (int c = 0; c < k; ++c) {
                     const double b = bt[(size_t)s * ldb + c];
-                    const double* e = &ws.Ex[(size_t)c * k];
+                    const double* e = &xs.Ex[(size_t)c * k];
                     for (int i = 0; i < k; ++i) y[i] += e[i] * b;
                 }
             }
+            return true;
+        };
+        const int nth = std::min(std::min(ws.nthreads, t), 4);
+        if (nth <= 1) {
+            for (int j = 0; j < t; ++j)
+                if (!term(j, ws.xs[0])) return false;
+        } else {
+            int top = 2;
+            for (int j = 0; j < t; ++j) top = std::max(top, ws.pw.needs(-alpha[j] * inv));
+            ws.pw.pw(top);
+            bool ok[4] = {true, true, true, true};
+            std::vector<std::thread> th;
+            for (int q = 1; q < nth; ++q)
+                th.emplace_back([&, q] {
+                    for (int j = q; j < t; j += nth) ok[q] = ok[q] && term(j, ws.xs[q]);
+                });
+            for (int j = 0; j < t; j += nth) ok[0] = ok[0] && term(j, ws.xs[0]);
+            for (auto& x : th) x.join();
+            for (int q = 0; q < nth; ++q)
+                if (!ok[q]) return false;
         }
     }
     return true;

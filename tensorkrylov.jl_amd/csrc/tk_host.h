@@ -15,16 +15,20 @@ bool sym_eig(int n, const double* A, int lda, Vec& w, Vec& Q);
 bool expm(int n, const double* A, Vec& E);
 
 // The even powers A^2..A^8 of one unscaled matrix, formed on demand and shared by every
-// exp(c A) of an iteration (tk_host.cpp expm_scaled), plus scratch.
+// exp(c A) of an iteration (tk_host.cpp expm_scaled); read-only once formed.
 struct ExpmPowers {
     int n = -1;
     const double* A = nullptr;
     double norm1 = 0.0;
     int have = 0;                       // highest even power formed (0, 2, 4, 6, 8)
     Vec P2, P4, P6, P8;
-    Vec U, V, T, Num, Den;              // scratch
     void reset(int n_, const double* A_);
     const double* pw(int k);            // A^k, k in {2, 4, 6, 8}
+    int needs(double c) const;          // the highest power exp(c A) reads
+};
+// per-thread scratch of one exp(c A)
+struct ExpmScratch {
+    Vec U, V, T, Num, Den, Ex;
 };
 
 // Scratch of the two functions below (grown on demand, reused across iterations).
@@ -32,6 +36,10 @@ struct Work {
     Vec w, Q, C, E, M, ec, G, Ex;
     Vec Z, Ly, Lz, X, pre, suf;
     ExpmPowers pw;
+    ExpmScratch xs[4];
+    // threads a nonsymmetric compressed solve may use for its exp-sum terms (the native loop
+    // raises it for the last iterations, when the other workers are idle)
+    int nthreads = 1;
 };
 
 // solve_compressed_system (src/tensor_krylov_method.jl:10-34): lambda[j] = omega[j]/lmin and

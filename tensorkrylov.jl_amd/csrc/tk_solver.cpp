@@ -365,6 +365,10 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
                 pool.cv.notify_all();
             }
         });
+    // the last two iterations run when every other evaluation is done or nearly so: their
+    // nonsymmetric exp-sum terms may take helper threads (Work::nthreads; bitwise the same)
+    const char* ets = getenv("TKHIP_SOLVER_TAIL_THREADS");
+    const int tail_threads = ets ? std::max(1, std::min(4, atoi(ets))) : 3;
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
@@ -372,6 +376,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         }
         {
             std::lock_guard<std::mutex> lk(workers[w].mu);
+            workers[w].ws.nthreads = k >= klast - 1 ? tail_threads : 1;
             workers[w].job = k;
         }
         workers[w].cv.notify_one();
