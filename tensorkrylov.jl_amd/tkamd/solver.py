@@ -189,7 +189,10 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
     covers the iterations only (the host mirror is copied back afterwards)."""
     device = hasattr(td.dev, "h") and hasattr(td.dev, "records")
     if device and pipelined:
+        import os
         nthr = threads or _native_threads()
+        # steps in flight ahead of the iteration being dispatched (TKHIP_SOLVER_DEPTH overrides)
+        depth = int(os.environ.get("TKHIP_SOLVER_DEPTH", depth))
         outcome, k_end, rel, proj, orth = sv.run(td.dev, tol, 2, max(depth, nthr + 1), nthr)
         conv.relative_residual_norm[1:k_end] = rel[1:k_end]
         conv.projected_residual_norm[1:k_end] = proj[1:k_end]
