@@ -687,15 +687,18 @@ struct tk_decomp {
     // what the caller enqueues next -- the flush + V*Y of the solve's end; a new sequence
     // (tk_decomp_init) waits for it before rewriting the basis
     hipEvent_t gev_in = nullptr, gev_done = nullptr;   // (the context's Gram stream)
-    // Factor groups (single rank, one-sweep Arnoldi, nf >= 2): local factors [0, g1) step on
-    // the compute stream and [g1, nf) on the context's fstream, each group in its own launches,
+    // Factor groups (one-sweep Arnoldi / Gram-free Lanczos, nf >= 2): the local factors step as
+    // 2 (default) or 3 groups, each on its own stream (grp_stream), each in its own launches,
     // so one group's launch drain and reduce overlap the other's sweep (two C2 halves on two
     // streams: 7 % less time than one 8-factor launch per step, tools/stream_probe.py).  The
     // streams fork at the first grouped step and join before anything else touches the
     // decomposition (fork_groups / join_groups).
-    int g1 = 0;                                    // 0: no groups
+    // ngr groups (1: none; TKHIP_FACTOR_GROUPS=3: three): group g steps local factors
+    // [gst[g], gst[g+1]) on grp_stream(g) -- the compute stream, fstream, gstream
+    int ngr = 1;
+    int gst[4] = {0, 0, 0, 0};
     bool forked = false;
-    hipEvent_t fev_fork = nullptr, fev_join = nullptr;
+    hipEvent_t fev_fork = nullptr, fev_join[2] = {nullptr, nullptr};
     bool gram_inflight = false;
     // the Gram launched ahead by tk_decomp_gram_ahead (0: none for this sequence): its column
     // count and the sequence number its host mirror publishes
@@ -780,7 +783,8 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->xdone) hipHostFree(dc->xdone);
     if (dc->cstream) hipStreamDestroy(dc->cstream);
     if (dc->fev_fork) hipEventDestroy(dc->fev_fork);
-    if (dc->fev_join) hipEventDestroy(dc->fev_join);
+    for (hipEvent_t e : dc->fev_join)
+        if (e) hipEventDestroy(e);
     if (dc->gev_in) hipEventDestroy(dc->gev_in);
     if (dc->gev_done) hipEventDestroy(dc->gev_done);
     delete dc;
@@ -1022,11 +1026,16 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         // words offset by the group's first factor), k_red_lan writes only device records
         const char* eg = getenv("TKHIP_FACTOR_GROUPS");
         const bool lan_ok = method == TK_LANCZOS && !dc->any_gram;
-        if ((dc->recv == dc->rec || dc->xflag) && (method == TK_ARNOLDI || lan_ok) && dc->onesweep && nf >= 2 &&
-            !(eg && eg[0] == '1') &&
-            hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess &&
-            hipEventCreateWithFlags(&dc->fev_join, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess)
-            dc->g1 = nf / 2;
+        const int want = eg ? std::max(1, std::min(3, atoi(eg))) : 2;
+        const int G = std::min(want, nf);
+        bool ok = G >= 2 && (dc->recv == dc->rec || dc->xflag) && (method == TK_ARNOLDI || lan_ok) && dc->onesweep &&
+                  hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
+        for (int g = 0; ok && g < G - 1; ++g)
+            ok = hipEventCreateWithFlags(&dc->fev_join[g], hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
+        if (ok) {
+            dc->ngr = G;
+            for (int g = 0; g <= G; ++g) dc->gst[g] = g * nf / G;
+        }
         (void)hipGetLastError();
     }
     {
@@ -1121,7 +1130,7 @@ int tk_decomp_matrix_reads(tk_decomp* dc) { return !dc ? -1 : (dc->mfspmv ? 1 : 
 
 int tk_decomp_gram_deferred(tk_decomp* dc) { return dc && dc->gram_deferred ? 1 : 0; }
 
-int tk_decomp_factor_groups(tk_decomp* dc) { return dc && dc->g1 > 0 ? 2 : 1; }
+int tk_decomp_factor_groups(tk_decomp* dc) { return dc ? dc->ngr : 1; }
 
 tk_status tk_decomp_set_replica(tk_decomp* dc, int replica) { TK_API_BEGIN
     CHECKARG(dc, "NULL handle");
@@ -1179,32 +1188,41 @@ tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     TK_API_END
 }
 
+// the stream of factor group g: the compute stream, then the context's fstream and gstream
+// (gstream carries the side-stream Gram only after the groups have joined)
+static hipStream_t grp_stream(tk_decomp* dc, int g) {
+    return g == 0 ? dc->ctx->stream : (g == 1 ? dc->ctx->fstream : dc->ctx->gstream);
+}
+
 // Before a slot's send rows are rewritten, the previous all-reduce of that slot must
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
     // (an already completed exchange needs no wait packet in the compute queue)
     if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess) {
         HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
-        // factor groups already forked: the second group's launches write their factors' rows
-        // of the slot from the other stream (a fork after this point inherits the wait)
-        if (dc->forked) HIPCHK(hipStreamWaitEvent(dc->ctx->fstream, dc->ev_x[dc->xev[slot]], 0));
+        // factor groups already forked: the other groups' launches write their factors' rows
+        // of the slot from their streams (a fork after this point inherits the wait)
+        for (int g = 1; dc->forked && g < dc->ngr; ++g)
+            HIPCHK(hipStreamWaitEvent(grp_stream(dc, g), dc->ev_x[dc->xev[slot]], 0));
     }
     return TK_OK;
 }
 
-// factor groups: the second group's stream starts after everything enqueued so far ...
+// factor groups: the other groups' streams start after everything enqueued so far ...
 static tk_status fork_groups(tk_decomp* dc) {
     if (dc->forked) return TK_OK;
     HIPCHK(hipEventRecord(dc->fev_fork, dc->ctx->stream));
-    HIPCHK(hipStreamWaitEvent(dc->ctx->fstream, dc->fev_fork, 0));
+    for (int g = 1; g < dc->ngr; ++g) HIPCHK(hipStreamWaitEvent(grp_stream(dc, g), dc->fev_fork, 0));
     dc->forked = true;
     return TK_OK;
 }
-// ... and the compute stream waits for it before any launch that is not a grouped step
+// ... and the compute stream waits for them before any launch that is not a grouped step
 static tk_status join_groups(tk_decomp* dc) {
     if (!dc->forked) return TK_OK;
-    HIPCHK(hipEventRecord(dc->fev_join, dc->ctx->fstream));
-    HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->fev_join, 0));
+    for (int g = 1; g < dc->ngr; ++g) {
+        HIPCHK(hipEventRecord(dc->fev_join[g - 1], grp_stream(dc, g)));
+        HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->fev_join[g - 1], 0));
+    }
     dc->forked = false;
     return TK_OK;
 }
@@ -1451,7 +1469,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         ax.seq = ++dc->seq;
     }
     Timer step_timer(c, TCLS_STEP, dc->in_sweep ? 99 : 1);
-    const bool grouped = dc->g1 > 0 && (dc->method == TK_ARNOLDI || (dc->method == TK_LANCZOS && !dc->any_gram)) &&
+    const bool grouped = dc->ngr > 1 && (dc->method == TK_ARNOLDI || (dc->method == TK_LANCZOS && !dc->any_gram)) &&
                          dc->onesweep && j <= ARN_D1_JMAX;
     if (!grouped) GJOIN(dc);
     if ((dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && j > ARN_D1_JMAX && dc->pending &&
@@ -1484,9 +1502,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             // of a group's launch serve that group's factors: host-mirror words offset by g0)
             tk_status stf = fork_groups(dc);
             if (stf) return stf;
-            for (int g = 0; g < 2; ++g) {
-                const int g0 = g ? dc->g1 : 0, ng = g ? nf - dc->g1 : dc->g1;
-                hipStream_t sg = g ? c->fstream : s;
+            for (int g = 0; g < dc->ngr; ++g) {
+                const int g0 = dc->gst[g], ng = dc->gst[g + 1] - dc->gst[g];
+                hipStream_t sg = grp_stream(dc, g);
                 KArgs bg = b;
                 if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                 {
@@ -1559,9 +1577,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 // previous step's records of that group's factors: host words offset by g0
                 tk_status stf = fork_groups(dc);
                 if (stf) return stf;
-                for (int g = 0; g < 2; ++g) {
-                    const int g0 = g ? dc->g1 : 0, ng = g ? nf - dc->g1 : dc->g1;
-                    hipStream_t sg = g ? c->fstream : s;
+                for (int g = 0; g < dc->ngr; ++g) {
+                    const int g0 = dc->gst[g], ng = dc->gst[g + 1] - dc->gst[g];
+                    hipStream_t sg = grp_stream(dc, g);
                     KArgs bg = b;
                     if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                     {
@@ -1772,7 +1790,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
                         // the device may have failed: surface its error instead of spinning (both
                         // factor-group streams: the records are late only if neither runs)
                         hipError_t e = hipStreamQuery(c->stream);
-                        if (e == hipSuccess && dc->g1 > 0) e = hipStreamQuery(c->fstream);
+                        for (int g = 1; e == hipSuccess && g < dc->ngr; ++g) e = hipStreamQuery(grp_stream(dc, g));
                         if (e != hipSuccess && e != hipErrorNotReady)
                             return fail(TK_ERR_HIP, "waiting for step records: %s", hipGetErrorString(e));
                         if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)

@@ -21,12 +21,12 @@ def test_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
     bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
     Ys = [rng.standard_normal((K, t)) for _ in range(d)]
     out = {}
-    for G in ("1", "2"):
+    for G in ("1", "2", "3"):
         monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
         A = [tk.DeviceMatrix(ctx, m) for m in mats]
         dev = tk.DeviceDecomposition(ctx, 0, d, 0, [A[s % 2] for s in range(d)], bs, K)
         assert dev.arnoldi_sweeps == 1
-        assert dev.factor_groups == int(G)
+        assert dev.factor_groups == min(int(G), d)
         r0 = dev.init()
         recs = [dev.step(j) for j in range(12)]          # one at a time, records read
         dev.sweep(12, K - 1)                             # the rest as a sweep
@@ -39,15 +39,16 @@ def test_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
         dev.close()
         for a in A:
             a.close()
-    (a0, ar, aa, aV, aX), (b0, br, ba, bV, bX) = out["1"], out["2"]
-    assert np.array_equal(a0, b0)
-    for x, y in zip(ar, br):
-        assert np.array_equal(x, y)
-    assert np.array_equal(aa, ba)
-    for x, y in zip(aV, bV):
-        assert np.array_equal(x, y)
-    for x, y in zip(aX, bX):
-        assert np.array_equal(x, y)
+    for G in ("2", "3"):
+        (a0, ar, aa, aV, aX), (b0, br, ba, bV, bX) = out["1"], out[G]
+        assert np.array_equal(a0, b0)
+        for x, y in zip(ar, br):
+            assert np.array_equal(x, y)
+        assert np.array_equal(aa, ba)
+        for x, y in zip(aV, bV):
+            assert np.array_equal(x, y)
+        for x, y in zip(aX, bX):
+            assert np.array_equal(x, y)
     # and the basis is an orthonormal Arnoldi basis
     assert np.abs(aV[0].T @ aV[0] - np.eye(K + 1)).max() < 1e-12
 
@@ -93,8 +94,13 @@ def test_factor_groups_under_records_exchange(ctx, grp, monkeypatch):
     monkeypatch.setenv("TKHIP_XCH_GROUP", grp)
     try:
         xch = run(c2, "2")
+        xch3 = run(c2, "3")
     finally:
         c2.close()
+    for a, b in zip(xch[1], xch3[1]):
+        assert np.array_equal(a, b)
+    for a, b in zip(xch[3], xch3[3]):
+        assert np.array_equal(a, b)
     assert np.array_equal(local[0], xch[0])
     for a, b in zip(local[1], xch[1]):
         assert np.array_equal(a, b)
@@ -117,12 +123,12 @@ def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
     bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
     Ys = [rng.standard_normal((K, t)) for _ in range(d)]
     out = {}
-    for G in ("1", "2"):
+    for G in ("1", "2", "3"):
         monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
         A = tk.DeviceMatrix(ctx, mat)
         dev = tk.DeviceDecomposition(ctx, tk._lib.TK_LANCZOS, d, 0, [A] * d, bs, K)
         assert dev.arnoldi_sweeps == 1 and dev.gram_deferred
-        assert dev.factor_groups == int(G)
+        assert dev.factor_groups == min(int(G), d)
         r0 = dev.init()
         recs = [dev.step(j) for j in range(9)]
         for j in range(9, 17):
@@ -136,11 +142,12 @@ def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
         out[G] = (r0, recs, V, X)
         dev.close()
         A.close()
-    (a0, ar, aV, aX), (b0, br, bV, bX) = out["1"], out["2"]
-    assert np.array_equal(a0, b0)
-    for x, y in zip(ar, br):
-        assert np.array_equal(x, y)
-    for x, y in zip(aV, bV):
-        assert np.array_equal(x, y)
-    for x, y in zip(aX, bX):
-        assert np.array_equal(x, y)
+    for G in ("2", "3"):
+        (a0, ar, aV, aX), (b0, br, bV, bX) = out["1"], out[G]
+        assert np.array_equal(a0, b0)
+        for x, y in zip(ar, br):
+            assert np.array_equal(x, y)
+        for x, y in zip(aV, bV):
+            assert np.array_equal(x, y)
+        for x, y in zip(aX, bX):
+            assert np.array_equal(x, y)

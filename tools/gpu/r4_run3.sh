@@ -8,7 +8,7 @@ grep -E "PASSED|FAILED|ERROR|passed|failed" gpurun_out/t_groups.log | tail -8
 timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -k lanczos_all_8 -x -v -s --timeout 500 --timeout-method thread > gpurun_out/t_c2lan.log 2>&1; rc=$?
 grep -E "C2 Lanczos|passed|failed|Error" gpurun_out/t_c2lan.log | tail -12
 [ $rc -eq 0 ] || exit 1
-for G in 1 2; do
+for G in 1 2 3; do
   TKHIP_FACTOR_GROUPS=$G timeout -k 10 300 python bench.py --no-cpu-baseline --method TensorLanczos --steps 10 --warmup 2 > gpurun_out/lan_g$G.log 2>&1 || { echo "lan G=$G failed"; tail -5 gpurun_out/lan_g$G.log; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/lan_g$G.log').read().strip().splitlines()[-1]); e=d['end_to_end']
