@@ -1024,8 +1024,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         // One-sweep Lanczos groups its Gram-free steps (k_lan_1w + k_red_lan) the same way:
         // each launch's bookkeeping blocks mirror and signal their own group's factors (host
         // words offset by the group's first factor), k_red_lan writes only device records
+        // (Lanczos groups are opt-in, TKHIP_LANCZOS_GROUPS=1: at C2 the grouped 77 us step ran
+        // 8 % slower -- each group's reduce queued behind the other group's window loads;
+        // profiles/r04/lanczos_groups_ab.txt)
         const char* eg = getenv("TKHIP_FACTOR_GROUPS");
-        const bool lan_ok = method == TK_LANCZOS && !dc->any_gram;
+        const char* elg = getenv("TKHIP_LANCZOS_GROUPS");
+        const bool lan_ok = method == TK_LANCZOS && !dc->any_gram && elg && elg[0] == '1';
         const int want = eg ? std::max(1, std::min(3, atoi(eg))) : 2;
         const int G = std::min(want, nf);
         bool ok = G >= 2 && (dc->recv == dc->rec || dc->xflag) && (method == TK_ARNOLDI || lan_ok) && dc->onesweep &&

@@ -295,6 +295,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
                         double* relres, double* projres, double* orth, int* k_end, int* outcome) { TK_API_BEGIN
     if (!sv || !dc || !relres || !projres || !orth || !k_end || !outcome || kfirst < 2)
         return tk_fail_internal(TK_ERR_ARG, "tk_solver_run: bad argument");
+    const auto t_entry = std::chrono::steady_clock::now();
     const int kmax = sv->kmax;
     int klast = kmax;   // iterations with a tabulated exp-sum rank
     for (int k = kfirst; k <= kmax; ++k)
@@ -471,9 +472,13 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         }
         if (k == klast) std::swap(sv->last, r);
     }
+    const auto t_loop_end = clk::now();
     stop_workers();
     if (etr) {
         if (FILE* f = fopen(etr, "w")) {
+            fprintf(f, "# entry_to_loop_us=%.1f loop_us=%.1f stop_workers_us=%.1f\n",
+                    std::chrono::duration<double, std::micro>(t_begin - t_entry).count(), since(t_loop_end),
+                    std::chrono::duration<double, std::micro>(clk::now() - t_loop_end).count());
             fprintf(f, "k,record_us,eval_start_us,eval_end_us,consumed_us\n");
             const double base = std::chrono::duration<double>(t_begin.time_since_epoch()).count();
             for (int k = kfirst; k <= *k_end; ++k)

@@ -193,7 +193,9 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
         nthr = threads or _native_threads()
         # steps in flight ahead of the iteration being dispatched (TKHIP_SOLVER_DEPTH overrides)
         depth = int(os.environ.get("TKHIP_SOLVER_DEPTH", depth))
+        t_run = time.perf_counter()
         outcome, k_end, rel, proj, orth = sv.run(td.dev, tol, 2, max(depth, nthr + 1), nthr)
+        conv.timing["native_run_s"] = time.perf_counter() - t_run
         conv.relative_residual_norm[1:k_end] = rel[1:k_end]
         conv.projected_residual_norm[1:k_end] = proj[1:k_end]
         conv.orthogonality_data[1:k_end] = orth[1:k_end]

@@ -117,6 +117,7 @@ def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
     sweep), the basis, the flushed column and V*Y bitwise those of one stream."""
     import tkamd as tk
     monkeypatch.delenv("TKHIP_GRAM", raising=False)
+    monkeypatch.setenv("TKHIP_LANCZOS_GROUPS", "1")   # (opt-in: slower at C2, DESIGN.md round 4)
     n, K, t = 3000, 40, 5
     rng = np.random.default_rng(78)
     mat = tk.assemble_matrix(n, "Laplace")

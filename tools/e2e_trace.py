@@ -6,7 +6,11 @@ usage: python tools/e2e_trace.py TRACE.csv [device_us_per_iteration]"""
 import csv
 import sys
 
-rows = [{k: float(v) for k, v in r.items()} for r in csv.DictReader(open(sys.argv[1]))]
+lines = open(sys.argv[1]).read().splitlines()
+if lines and lines[0].startswith("#"):
+    print("native loop:", lines[0][1:].strip())
+    lines = lines[1:]
+rows = [{k: float(v) for k, v in r.items()} for r in csv.DictReader(lines)]
 dev = float(sys.argv[2]) if len(sys.argv) > 2 else None
 ks = [int(r["k"]) for r in rows]
 rec = [r["record_us"] for r in rows]

@@ -10,3 +10,4 @@ print('rep $rep $cfg G=$G', d['value'], 'frac', d['roofline']['frac'], 'groups',
 done; done; done
 bash tools/gpu/r4_xmap.sh || exit 1
 bash tools/gpu/r4_c3.sh
+bash tools/gpu/r4_e2e.sh

@@ -16,5 +16,5 @@ tr c4 --config C4
 tr c2e8 --emulate-ranks 8
 tr c4e8r7 --config C4 --emulate-ranks 8 --emulate-rank 7
 tr c2 
-TKHIP_SOLVER_DEPTH=24 tr c2e8_d24 --emulate-ranks 8
-TKHIP_SOLVER_DEPTH=24 tr c4_d24 --config C4
+
+
