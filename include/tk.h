@@ -320,6 +320,10 @@ tk_status tk_solver_state(tk_solver* sv, double* H_out, double* bt_out, double* 
  * (slot = j + 1, kmax + 2 slots), so one GPU holding one rank's factors drives the same
  * iterates as the whole job.  records = NULL removes the overlay. */
 tk_status tk_solver_overlay(tk_solver* sv, int first, int nf, const double* records);
+/* Start the native loop's evaluation threads ahead of tk_solver_run (the driver's setup): at
+ * least nthreads workers, kept by the solver until tk_solver_destroy (a run needing more --
+ * the agreed worker count -- starts the rest itself). */
+tk_status tk_solver_prepare(tk_solver* sv, int nthreads);
 /* The pipelined loop for k = kfirst .. kmax on a decomposition whose steps < kfirst-1 are
  * done and applied: enqueues steps up to `depth` ahead, applies each step's records in
  * order and evaluates up to `nthreads` iterations concurrently on host threads (each

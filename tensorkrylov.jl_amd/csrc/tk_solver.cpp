@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -49,6 +50,26 @@ struct IterResult {
     Vec lam, Y;                   // lambda (t), Y [d][t][k]
 };
 
+// ------------------------------------------------------------------ worker pool
+// Idle workers block (the box's CPU share is a cgroup quota: spinning threads would spend
+// it); a job is handed over under the worker's mutex, its completion under the pool's.  The
+// threads belong to the solver: started ahead of the loop (tk_solver_prepare, the driver's
+// setup) or by its first run, kept until tk_solver_destroy.
+struct Worker {
+    std::mutex mu;
+    std::condition_variable cv;
+    int job = 0;                  // iteration to evaluate, 0 = idle, -1 = exit
+    IterResult res;
+    Work ws;
+    std::thread th;
+};
+
+struct Pool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> done;        // per worker: iteration whose result is ready
+};
+
 }  // namespace
 
 struct tk_solver {
@@ -70,6 +91,8 @@ struct tk_solver {
     // ov_first + ov_nf) are taken from records recorded by a full run, [slot][d][m]
     std::vector<double> overlay;
     int ov_first = 0, ov_nf = 0;
+    Pool pool;
+    std::vector<std::unique_ptr<Worker>> workers;
 };
 
 static void apply_record(tk_solver* sv, int j, const double* rec) {
@@ -165,31 +188,65 @@ static void evaluate(const tk_solver* sv, int k, IterResult& out, Work& ws) {
     out.orth = sqrt(acc);
 }
 
-// ------------------------------------------------------------------ worker pool
-// Idle workers block (the box's CPU share is a cgroup quota: spinning threads would spend
-// it); a job is handed over under the worker's mutex, its completion under the pool's.
-namespace {
+static void worker_loop(tk_solver* sv, int w, Worker* wkp) {
+    Worker& wk = *wkp;
+    for (;;) {
+        int k;
+        {
+            std::unique_lock<std::mutex> lk(wk.mu);
+            wk.cv.wait(lk, [&] { return wk.job != 0; });
+            k = wk.job;
+        }
+        if (k < 0) return;
+        const double tb = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        evaluate(sv, k, wk.res, wk.ws);
+        wk.res.t0 = tb;
+        wk.res.t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        {
+            std::lock_guard<std::mutex> lk(wk.mu);
+            wk.job = 0;
+        }
+        {
+            std::lock_guard<std::mutex> lk(sv->pool.mu);
+            sv->pool.done[w] = k;
+        }
+        sv->pool.cv.notify_all();
+    }
+}
 
-struct Pool;
+// at least P worker threads (only between runs: no job is in flight)
+static void start_workers(tk_solver* sv, int P) {
+    {
+        std::lock_guard<std::mutex> lk(sv->pool.mu);
+        if ((int)sv->pool.done.size() < P) sv->pool.done.resize(P, 0);
+    }
+    while ((int)sv->workers.size() < P) {
+        Worker* wk = new Worker();
+        sv->workers.emplace_back(wk);
+        wk->th = std::thread(worker_loop, sv, (int)sv->workers.size() - 1, wk);
+    }
+}
 
-struct Worker {
-    std::mutex mu;
-    std::condition_variable cv;
-    int job = 0;                  // iteration to evaluate, 0 = idle, -1 = exit
-    IterResult res;
-    Work ws;
-    std::thread th;
-};
-
-struct Pool {
-    std::mutex mu;
-    std::condition_variable cv;
-    std::vector<int> done;        // per worker: iteration whose result is ready
-};
-
-}  // namespace
+static void stop_workers(tk_solver* sv) {
+    for (auto& wk : sv->workers) {
+        {
+            std::lock_guard<std::mutex> lk(wk->mu);
+            wk->job = -1;
+        }
+        wk->cv.notify_one();
+    }
+    for (auto& wk : sv->workers) wk->th.join();
+    sv->workers.clear();
+}
 
 extern "C" {
+
+tk_status tk_solver_prepare(tk_solver* sv, int nthreads) { TK_API_BEGIN
+    if (!sv || nthreads < 1) return tk_fail_internal(TK_ERR_ARG, "tk_solver_prepare: bad argument");
+    start_workers(sv, std::min(nthreads, 64));
+    return TK_OK;
+    TK_API_END
+}
 
 tk_status tk_solver_create(int method, int d, int kmax, int symmetric, double b_norm, const double* lmin,
                            const int* rank, const double* alpha, const double* omega, tk_solver** out) { TK_API_BEGIN
@@ -242,6 +299,8 @@ tk_status tk_solver_overlay(tk_solver* sv, int first, int nf, const double* reco
 }
 
 tk_status tk_solver_destroy(tk_solver* sv) {
+    if (!sv) return TK_OK;
+    stop_workers(sv);
     delete sv;
     return TK_OK;
 }
@@ -338,34 +397,13 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     if (!st) st = ahead();
     if (st) return st;
 
-    std::vector<Worker> workers(P);
-    Pool pool;
-    pool.done.assign(P, 0);
-    for (int w = 0; w < P; ++w)
-        workers[w].th = std::thread([sv, w, &wk = workers[w], &pool] {
-            for (;;) {
-                int k;
-                {
-                    std::unique_lock<std::mutex> lk(wk.mu);
-                    wk.cv.wait(lk, [&] { return wk.job != 0; });
-                    k = wk.job;
-                }
-                if (k < 0) return;
-                const double tb = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-                evaluate(sv, k, wk.res, wk.ws);
-                wk.res.t0 = tb;
-                wk.res.t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
-                {
-                    std::lock_guard<std::mutex> lk(wk.mu);
-                    wk.job = 0;
-                }
-                {
-                    std::lock_guard<std::mutex> lk(pool.mu);
-                    pool.done[w] = k;
-                }
-                pool.cv.notify_all();
-            }
-        });
+    start_workers(sv, P);
+    auto& workers = sv->workers;
+    Pool& pool = sv->pool;
+    {
+        std::lock_guard<std::mutex> lk(pool.mu);
+        for (auto& x : pool.done) x = 0;
+    }
     // the last two iterations run when every other evaluation is done or nearly so: their
     // nonsymmetric exp-sum terms may take helper threads (Work::nthreads; bitwise the same)
     const char* ets = getenv("TKHIP_SOLVER_TAIL_THREADS");
@@ -376,33 +414,28 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             pool.done[w] = 0;
         }
         {
-            std::lock_guard<std::mutex> lk(workers[w].mu);
-            workers[w].ws.nthreads = k >= klast - 1 ? tail_threads : 1;
-            workers[w].job = k;
+            std::lock_guard<std::mutex> lk(workers[w]->mu);
+            workers[w]->ws.nthreads = k >= klast - 1 ? tail_threads : 1;
+            workers[w]->job = k;
         }
-        workers[w].cv.notify_one();
+        workers[w]->cv.notify_one();
     };
     auto wait_done = [&](int w, int k) {
         std::unique_lock<std::mutex> lk(pool.mu);
         pool.cv.wait(lk, [&] { return pool.done[w] == k; });
     };
-    auto stop_workers = [&] {
+    // the end of a run: jobs still in flight finish (their results are discarded); the
+    // threads stay for the next run or tk_solver_destroy
+    auto quiesce = [&] {
         for (auto& wk : workers) {
-            {
-                std::unique_lock<std::mutex> lk(wk.mu);
-                // a job still in flight finishes first (its result is discarded)
-                while (wk.job > 0) {
-                    lk.unlock();
-                    std::this_thread::yield();
-                    lk.lock();
-                }
-                wk.job = -1;
+            std::unique_lock<std::mutex> lk(wk->mu);
+            while (wk->job > 0) {
+                lk.unlock();
+                std::this_thread::yield();
+                lk.lock();
             }
-            wk.cv.notify_one();
         }
-        for (auto& wk : workers) wk.th.join();
     };
-
     int k_dispatch = kfirst;
     tk_status err = TK_OK;
     // TKHIP_SOLVER_STATS=1: where the calling thread's time goes (stderr)
@@ -423,7 +456,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     const char* etr = getenv("TKHIP_SOLVER_TRACE");
     std::vector<double> tr_rec(kmax + 2, -1.0), tr_cons(kmax + 2, -1.0);
     auto since = [&](clk::time_point p) { return std::chrono::duration<double, std::micro>(p - t_begin).count(); };
-    for (auto& wk : workers) wk.res.t0 = wk.res.t1 = -1.0;
+    for (auto& wk : workers) wk->res.t0 = wk->res.t1 = -1.0;
     std::vector<double> tr_e0(kmax + 2, -1.0), tr_e1(kmax + 2, -1.0);
     for (int k = kfirst; k <= klast; ++k) {
         // keep P evaluations in flight: records of step k_dispatch-1, applied in order
@@ -442,7 +475,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             lap(t_apply);
         }
         if (err) break;
-        Worker& wk = workers[(k - kfirst) % P];
+        Worker& wk = *workers[(k - kfirst) % P];
         wait_done((k - kfirst) % P, k);
         lap(t_wait);
         IterResult& r = wk.res;
@@ -473,10 +506,10 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         if (k == klast) std::swap(sv->last, r);
     }
     const auto t_loop_end = clk::now();
-    stop_workers();
+    quiesce();
     if (etr) {
         if (FILE* f = fopen(etr, "w")) {
-            fprintf(f, "# entry_to_loop_us=%.1f loop_us=%.1f stop_workers_us=%.1f\n",
+            fprintf(f, "# entry_to_loop_us=%.1f loop_us=%.1f quiesce_us=%.1f\n",
                     std::chrono::duration<double, std::micro>(t_begin - t_entry).count(), since(t_loop_end),
                     std::chrono::duration<double, std::micro>(clk::now() - t_loop_end).count());
             fprintf(f, "k,record_us,eval_start_us,eval_end_us,consumed_us\n");

@@ -323,6 +323,10 @@ class NativeSolver:
                                                     self._L.dptr(G)))
         return H, bt, G
 
+    def prepare(self, nthreads):
+        """Start the evaluation threads now (setup), not inside the loop (tk_solver_prepare)."""
+        self._L.check(self._L.lib().tk_solver_prepare(self.h, int(nthreads)))
+
     def run(self, dev, tol, kfirst=2, depth=2, nthreads=4):
         """Pipelined loop k = kfirst..kmax on a DeviceDecomposition.  Returns (outcome,
         k_end, relres, projres, orth) with outcome 0 / 1 / 2 as tk_solver_run."""

@@ -69,6 +69,8 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             tables = IterationTables(A, nmax, tol, d)
             conv.timing["tables_s"] = time.perf_counter() - t_tab
             sv = NativeSolver(td.method, d, nmax, symmetric, b_norm, tables)
+            if pipelined and hasattr(td.dev, "h"):
+                sv.prepare(threads or _native_threads())   # (worker threads: setup, not loop)
             try:
                 if overlay is not None:
                     sv.overlay(td.part.first, td.part.nf, overlay)
