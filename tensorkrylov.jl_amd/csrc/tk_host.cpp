@@ -537,7 +537,20 @@ bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, co
                 const double* cs = &ws.C[(size_t)s * k];
                 for (int c = 0; c < k; ++c) m[c] = e[c] * cs[c];
             }
-        gemm_nn(k, t * d, k, Q, k, ws.M.data(), k, Y, k);
+        // (with helper threads: column blocks of Y = Q M, each column the same arithmetic)
+        const int ncol = t * d, nth = std::min(std::min(ws.nthreads, 4), ncol / 8);
+        if (nth <= 1) {
+            gemm_nn(k, ncol, k, Q, k, ws.M.data(), k, Y, k);
+        } else {
+            std::vector<std::thread> th;
+            auto part = [&](int q) {
+                const int c0 = q * ncol / nth, c1 = (q + 1) * ncol / nth;
+                gemm_nn(k, c1 - c0, k, Q, k, ws.M.data() + (size_t)c0 * k, k, Y + (size_t)c0 * k, k);
+            };
+            for (int q = 1; q < nth; ++q) th.emplace_back(part, q);
+            part(0);
+            for (auto& x : th) x.join();
+        }
     } else {
         // every term exp(g_j H1) from the same powers of H1 (ExpmPowers); with ws.nthreads > 1
         // the terms are spread over threads (the powers formed first, then read-only; each
@@ -593,9 +606,10 @@ int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const dou
     ws.Ly.assign(d * tt, 0.0);
     ws.Lz.assign(d * tt, 0.0);
     ws.X.assign(d * tt, 0.0);
-    ws.G.resize((size_t)4 * tt);
-    ws.M.resize((size_t)2 * kt);
-    for (int s = 0; s < d; ++s) {
+    // per factor: Z_s = H_s Y_s and the Gram blocks of [Y_s Z_s]; independent over s, so with
+    // helper threads (ws.nthreads) the factors are split over them (each factor's arithmetic
+    // unchanged; scratch per thread)
+    auto factor = [&](int s, Vec& G2, Vec& YZv, Vec& tmp) {
         const double* Hs = H + (size_t)s * hs;
         double* Zs = &ws.Z[(size_t)s * kt];
         const double* Ys = Y + (size_t)s * kt;
@@ -603,14 +617,14 @@ int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const dou
         // is still cheaper than a column-by-column band update)
         gemm_nn(k, t, k, Hs, ldh, Ys, k, Zs, k);
         // G = [Y Z]' [Y Z]  (2t x 2t, row-major): Ly = lower(G11), X = G12, Lz = lower(G22)
-        double* YZ = ws.M.data();
+        double* YZ = YZv.data();
         memcpy(YZ, Ys, kt * sizeof(double));
         memcpy(YZ + kt, Zs, kt * sizeof(double));
-        gemm_tn(2 * t, 2 * t, k, YZ, YZ, ws.G.data(), 2 * t, ws.Ex);
+        gemm_tn(2 * t, 2 * t, k, YZ, YZ, G2.data(), 2 * t, tmp);
         double* Ly = &ws.Ly[s * tt];
         double* Lz = &ws.Lz[s * tt];
         double* X = &ws.X[s * tt];
-        const double* G = ws.G.data();
+        const double* G = G2.data();
         for (int i = 0; i < t; ++i)
             for (int j = 0; j < t; ++j) {
                 X[(size_t)i * t + j] = G[(size_t)i * 2 * t + t + j];
@@ -619,6 +633,21 @@ int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const dou
                     Lz[(size_t)i * t + j] = G[(size_t)(t + i) * 2 * t + t + j];
                 }
             }
+    };
+    ws.G.resize((size_t)4 * tt);
+    ws.M.resize((size_t)2 * kt);
+    const int nth = std::min(std::min(ws.nthreads, 4), d);
+    if (nth <= 1) {
+        for (int s = 0; s < d; ++s) factor(s, ws.G, ws.M, ws.Ex);
+    } else {
+        std::vector<std::thread> th;
+        auto part = [&](int q) {
+            Vec G2((size_t)4 * tt), YZv((size_t)2 * kt), tmp;
+            for (int s = q; s < d; s += nth) factor(s, G2, YZv, tmp);
+        };
+        for (int q = 1; q < nth; ++q) th.emplace_back(part, q);
+        part(0);
+        for (auto& x : th) x.join();
     }
     auto W = [&](int i, int j) { return i == j ? 1.0 : 2.0; };   // lower triangle only
     // first term: sum_s beta_s^2 * sum W .* Gamma_s .* prod_{q != s} Ly_q  (prefix/suffix)

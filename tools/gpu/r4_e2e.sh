@@ -18,3 +18,6 @@ tr c4e8r7 --config C4 --emulate-ranks 8 --emulate-rank 7
 tr c2 
 
 
+TKHIP_SOLVER_TAIL_THREADS=1 tr c4_tail1 --config C4
+TKHIP_SOLVER_TAIL_THREADS=1 tr c4e8r7_tail1 --config C4 --emulate-ranks 8 --emulate-rank 7
+TKHIP_SOLVER_TAIL_THREADS=1 tr c1_tail1 --config C1
