@@ -405,9 +405,11 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         for (auto& x : pool.done) x = 0;
     }
     // the last two iterations run when every other evaluation is done or nearly so: their
-    // nonsymmetric exp-sum terms may take helper threads (Work::nthreads; bitwise the same)
+    // nonsymmetric exp-sum terms may take helper threads (Work::nthreads; bitwise the same).
+    // Opt-in: on the MI355X box's host the spawn cost outweighed the split (tail C4 476 vs
+    // 227 us, C1 330 vs 122 us at 3 vs 1 thread; profiles/r04/e2e_traces_tail_threads_ab.txt)
     const char* ets = getenv("TKHIP_SOLVER_TAIL_THREADS");
-    const int tail_threads = ets ? std::max(1, std::min(4, atoi(ets))) : 3;
+    const int tail_threads = ets ? std::max(1, std::min(4, atoi(ets))) : 1;
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
