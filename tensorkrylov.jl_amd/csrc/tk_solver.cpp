@@ -315,6 +315,8 @@ tk_status tk_solver_apply(tk_solver* sv, int j, const double* rec) { TK_API_BEGI
 tk_status tk_solver_evaluate(tk_solver* sv, int k, double* out4) { TK_API_BEGIN
     if (!sv || !out4 || k < 2 || k > sv->kmax || sv->rank[k - 1] < 1)
         return tk_fail_internal(TK_ERR_ARG, "tk_solver_evaluate: bad argument");
+    // (TKHIP_EVAL_THREADS: helper threads of this single evaluation -- timing tools)
+    if (const char* e = getenv("TKHIP_EVAL_THREADS")) sv->ws.nthreads = std::max(1, std::min(4, atoi(e)));
     evaluate(sv, k, sv->last, sv->ws);
     out4[0] = sv->last.r_comp;
     out4[1] = sv->last.r_norm;
