@@ -21,7 +21,6 @@
 
 #include <algorithm>
 #include <new>
-#include <thread>
 #include <vector>
 
 #include "../../include/tk.h"
@@ -537,24 +536,17 @@ bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, co
                 const double* cs = &ws.C[(size_t)s * k];
                 for (int c = 0; c < k; ++c) m[c] = e[c] * cs[c];
             }
-        // (with helper threads: column blocks of Y = Q M, each column the same arithmetic)
-        const int ncol = t * d, nth = std::min(std::min(ws.nthreads, 4), ncol / 8);
-        if (nth <= 1) {
-            gemm_nn(k, ncol, k, Q, k, ws.M.data(), k, Y, k);
-        } else {
-            std::vector<std::thread> th;
-            auto part = [&](int q) {
-                const int c0 = q * ncol / nth, c1 = (q + 1) * ncol / nth;
-                gemm_nn(k, c1 - c0, k, Q, k, ws.M.data() + (size_t)c0 * k, k, Y + (size_t)c0 * k, k);
-            };
-            for (int q = 1; q < nth; ++q) th.emplace_back(part, q);
-            part(0);
-            for (auto& x : th) x.join();
-        }
+        // (with helpers: column blocks of Y = Q M, each column the same arithmetic)
+        const int ncol = t * d, nth = std::max(1, std::min(std::min(ws.nthreads, 4), ncol / 8));
+        auto part = [&](int q) {
+            const int c0 = q * ncol / nth, c1 = (q + 1) * ncol / nth;
+            gemm_nn(k, c1 - c0, k, Q, k, ws.M.data() + (size_t)c0 * k, k, Y + (size_t)c0 * k, k);
+        };
+        par_for(ws.par, nth, part);
     } else {
         // every term exp(g_j H1) from the same powers of H1 (ExpmPowers); with ws.nthreads > 1
-        // the terms are spread over threads (the powers formed first, then read-only; each
-        // term's arithmetic is the same whichever thread runs it)
+        // the terms are spread over helper tasks (the powers formed first, then read-only;
+        // each term's arithmetic is the same whichever thread runs it)
         ws.G.resize((size_t)k * k);
         for (int c = 0; c < k; ++c)
             for (int i = 0; i < k; ++i) ws.G[(size_t)c * k + i] = H1[(size_t)c * ldh + i];
@@ -582,13 +574,10 @@ bool compressed_solve(int d, int k, const double* H1, int ldh, int symmetric, co
             for (int j = 0; j < t; ++j) top = std::max(top, ws.pw.needs(-alpha[j] * inv));
             ws.pw.pw(top);
             bool ok[4] = {true, true, true, true};
-            std::vector<std::thread> th;
-            for (int q = 1; q < nth; ++q)
-                th.emplace_back([&, q] {
-                    for (int j = q; j < t; j += nth) ok[q] = ok[q] && term(j, ws.xs[q]);
-                });
-            for (int j = 0; j < t; j += nth) ok[0] = ok[0] && term(j, ws.xs[0]);
-            for (auto& x : th) x.join();
+            auto part = [&](int q) {
+                for (int j = q; j < t; j += nth) ok[q] = ok[q] && term(j, ws.xs[q]);
+            };
+            par_for(ws.par, nth, part);
             for (int q = 0; q < nth; ++q)
                 if (!ok[q]) return false;
         }
@@ -634,21 +623,15 @@ int residual(int d, int k, int t, const double* H, int ldh, size_t hs, const dou
                 }
             }
     };
-    ws.G.resize((size_t)4 * tt);
-    ws.M.resize((size_t)2 * kt);
-    const int nth = std::min(std::min(ws.nthreads, 4), d);
-    if (nth <= 1) {
-        for (int s = 0; s < d; ++s) factor(s, ws.G, ws.M, ws.Ex);
-    } else {
-        std::vector<std::thread> th;
-        auto part = [&](int q) {
-            Vec G2((size_t)4 * tt), YZv((size_t)2 * kt), tmp;
-            for (int s = q; s < d; s += nth) factor(s, G2, YZv, tmp);
-        };
-        for (int q = 1; q < nth; ++q) th.emplace_back(part, q);
-        part(0);
-        for (auto& x : th) x.join();
+    const int nth = std::max(1, std::min(std::min(ws.nthreads, 4), d));
+    for (int q = 0; q < nth; ++q) {
+        ws.G2[q].resize((size_t)4 * tt);
+        ws.YZ[q].resize((size_t)2 * kt);
     }
+    auto part = [&](int q) {
+        for (int s = q; s < d; s += nth) factor(s, ws.G2[q], ws.YZ[q], ws.tmp[q]);
+    };
+    par_for(ws.par, nth, part);
     auto W = [&](int i, int j) { return i == j ? 1.0 : 2.0; };   // lower triangle only
     // first term: sum_s beta_s^2 * sum W .* Gamma_s .* prod_{q != s} Ly_q  (prefix/suffix)
     ws.pre.assign(d * tt, 1.0);

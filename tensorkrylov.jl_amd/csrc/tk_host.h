@@ -31,15 +31,34 @@ struct ExpmScratch {
     Vec U, V, T, Num, Den, Ex;
 };
 
+// The data-parallel parts of one evaluation (exp-sum terms, column blocks of Y = Q M, the
+// residual's factors): run(n, fn, ctx) calls fn(ctx, i) for every i < n on the calling thread
+// and whichever helper threads are free, and returns when all n calls are done.  A task's
+// arithmetic depends on i alone, so the result is bitwise the serial one.
+struct ParFor {
+    virtual ~ParFor() {}
+    virtual void run(int n, void (*fn)(void*, int), void* ctx) = 0;
+};
+template <class F>
+inline void par_for(ParFor* p, int n, F& f) {
+    if (!p || n <= 1) {
+        for (int i = 0; i < n; ++i) f(i);
+        return;
+    }
+    p->run(n, [](void* c, int i) { (*static_cast<F*>(c))(i); }, &f);
+}
+
 // Scratch of the two functions below (grown on demand, reused across iterations).
 struct Work {
     Vec w, Q, C, E, M, ec, G, Ex;
     Vec Z, Ly, Lz, X, pre, suf;
+    Vec G2[4], YZ[4], tmp[4];
     ExpmPowers pw;
     ExpmScratch xs[4];
-    // threads a nonsymmetric compressed solve may use for its exp-sum terms (the native loop
-    // raises it for the last iterations, when the other workers are idle)
+    // tasks (<= 4) the parts above are split into, and the helpers that run them (the native
+    // loop sets both for the last iterations, when the other workers are idle)
     int nthreads = 1;
+    ParFor* par = nullptr;
 };
 
 // solve_compressed_system (src/tensor_krylov_method.jl:10-34): lambda[j] = omega[j]/lmin and

@@ -18,7 +18,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -70,6 +73,119 @@ struct Pool {
     std::vector<int> done;        // per worker: iteration whose result is ready
 };
 
+// Helper threads for the last iterations' evaluations (tkh::ParFor): persistent, so a split
+// costs a wake-up, not a thread start (a std::thread per split cost more than it saved:
+// C4 tail 476 vs 227 us, profiles/r04/e2e_traces_tail_threads_ab.txt).  Idle helpers block;
+// while `hot` (set by the loop when the tail iterations are dispatched) they spin instead,
+// so the split finds them running.  One split at a time: a second caller (two workers in
+// the tail together) runs its tasks itself.
+class Helpers : public ParFor {
+  public:
+    explicit Helpers(int nh) {
+        for (int i = 0; i < nh; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~Helpers() override {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            quit_.store(true);
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    void set_hot(bool h) {
+        if (hot_.exchange(h) == h || !h) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            ++wake_;
+        }
+        cv_.notify_all();
+    }
+    void run(int n, void (*fn)(void*, int), void* ctx) override {
+        std::unique_lock<std::mutex> own(call_mu_, std::try_to_lock);
+        if (!own.owns_lock() || th_.empty()) {
+            for (int i = 0; i < n; ++i) fn(ctx, i);
+            return;
+        }
+        Job j;
+        j.fn = fn;
+        j.ctx = ctx;
+        j.n = n;
+        j.left.store(n, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cur_ = &j;
+            posted_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        take(j);
+        while (j.left.load(std::memory_order_acquire) > 0) _mm_pause();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            cur_ = nullptr;
+        }
+        // (a helper that picked the job up may still be between its last task and leaving)
+        while (j.refs.load(std::memory_order_acquire) > 0) _mm_pause();
+    }
+
+  private:
+    struct Job {
+        void (*fn)(void*, int) = nullptr;
+        void* ctx = nullptr;
+        int n = 0;
+        std::atomic<int> next{0}, left{0}, refs{0};
+    };
+    static void take(Job& j) {
+        for (int i; (i = j.next.fetch_add(1, std::memory_order_relaxed)) < j.n;) {
+            j.fn(j.ctx, i);
+            j.left.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    void loop() {
+        unsigned seen = 0, wseen = 0;
+        for (;;) {
+            for (int spin = 0;;) {
+                if (quit_.load(std::memory_order_acquire)) return;
+                if (posted_.load(std::memory_order_acquire) != seen) break;
+                if (hot_.load(std::memory_order_relaxed) || ++spin < 4096) {
+                    _mm_pause();
+                    continue;
+                }
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return quit_.load() || posted_.load() != seen || wake_ != wseen; });
+                wseen = wake_;
+                spin = 0;
+            }
+            Job* j;
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                seen = posted_.load(std::memory_order_relaxed);
+                j = cur_;
+                if (j) j->refs.fetch_add(1, std::memory_order_relaxed);
+            }
+            if (!j) continue;
+            take(*j);
+            j->refs.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, call_mu_;
+    std::condition_variable cv_;
+    Job* cur_ = nullptr;
+    std::atomic<unsigned> posted_{0};
+    std::atomic<bool> hot_{false}, quit_{false};
+    unsigned wake_ = 0;
+};
+
+// TKHIP_SOLVER_TAIL_THREADS: tasks (1..4) the last two iterations' evaluations split into
+static int tail_threads() {
+    static const int v = [] {
+        const char* e = getenv("TKHIP_SOLVER_TAIL_THREADS");
+        return e ? std::max(1, std::min(4, atoi(e))) : 1;
+    }();
+    return v;
+}
+
 }  // namespace
 
 struct tk_solver {
@@ -93,6 +209,7 @@ struct tk_solver {
     int ov_first = 0, ov_nf = 0;
     Pool pool;
     std::vector<std::unique_ptr<Worker>> workers;
+    std::unique_ptr<Helpers> helpers;   // (tail_threads() > 1)
 };
 
 static void apply_record(tk_solver* sv, int j, const double* rec) {
@@ -225,6 +342,7 @@ static void start_workers(tk_solver* sv, int P) {
         sv->workers.emplace_back(wk);
         wk->th = std::thread(worker_loop, sv, (int)sv->workers.size() - 1, wk);
     }
+    if (tail_threads() > 1 && !sv->helpers) sv->helpers.reset(new Helpers(tail_threads() - 1));
 }
 
 static void stop_workers(tk_solver* sv) {
@@ -237,6 +355,7 @@ static void stop_workers(tk_solver* sv) {
     }
     for (auto& wk : sv->workers) wk->th.join();
     sv->workers.clear();
+    sv->helpers.reset();
 }
 
 extern "C" {
@@ -315,8 +434,12 @@ tk_status tk_solver_apply(tk_solver* sv, int j, const double* rec) { TK_API_BEGI
 tk_status tk_solver_evaluate(tk_solver* sv, int k, double* out4) { TK_API_BEGIN
     if (!sv || !out4 || k < 2 || k > sv->kmax || sv->rank[k - 1] < 1)
         return tk_fail_internal(TK_ERR_ARG, "tk_solver_evaluate: bad argument");
-    // (TKHIP_EVAL_THREADS: helper threads of this single evaluation -- timing tools)
-    if (const char* e = getenv("TKHIP_EVAL_THREADS")) sv->ws.nthreads = std::max(1, std::min(4, atoi(e)));
+    // (TKHIP_EVAL_THREADS: tasks of this single evaluation, on helper threads -- timing tools)
+    if (const char* e = getenv("TKHIP_EVAL_THREADS")) {
+        sv->ws.nthreads = std::max(1, std::min(4, atoi(e)));
+        if (sv->ws.nthreads > 1 && !sv->helpers) sv->helpers.reset(new Helpers(sv->ws.nthreads - 1));
+        sv->ws.par = sv->helpers.get();
+    }
     evaluate(sv, k, sv->last, sv->ws);
     out4[0] = sv->last.r_comp;
     out4[1] = sv->last.r_norm;
@@ -407,19 +530,20 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         for (auto& x : pool.done) x = 0;
     }
     // the last two iterations run when every other evaluation is done or nearly so: their
-    // nonsymmetric exp-sum terms may take helper threads (Work::nthreads; bitwise the same).
-    // Opt-in: on the MI355X box's host the spawn cost outweighed the split (tail C4 476 vs
-    // 227 us, C1 330 vs 122 us at 3 vs 1 thread; profiles/r04/e2e_traces_tail_threads_ab.txt)
-    const char* ets = getenv("TKHIP_SOLVER_TAIL_THREADS");
-    const int tail_threads = ets ? std::max(1, std::min(4, atoi(ets))) : 1;
+    // data-parallel parts may be split over the helper threads (Work::nthreads, Work::par;
+    // bitwise the same), which spin from the dispatch of iteration klast-2 on
+    Helpers* hp = sv->helpers.get();
+    const int tail = hp ? tail_threads() : 1;
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
             pool.done[w] = 0;
         }
+        if (hp && k >= klast - 2) hp->set_hot(true);
         {
             std::lock_guard<std::mutex> lk(workers[w]->mu);
-            workers[w]->ws.nthreads = k >= klast - 1 ? tail_threads : 1;
+            workers[w]->ws.nthreads = k >= klast - 1 ? tail : 1;
+            workers[w]->ws.par = hp;
             workers[w]->job = k;
         }
         workers[w]->cv.notify_one();
@@ -510,12 +634,14 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         if (k == klast) std::swap(sv->last, r);
     }
     const auto t_loop_end = clk::now();
+    if (hp) hp->set_hot(false);
     quiesce();
+    const auto t_quiet = clk::now();
     if (etr) {
         if (FILE* f = fopen(etr, "w")) {
             fprintf(f, "# entry_to_loop_us=%.1f loop_us=%.1f quiesce_us=%.1f\n",
                     std::chrono::duration<double, std::micro>(t_begin - t_entry).count(), since(t_loop_end),
-                    std::chrono::duration<double, std::micro>(clk::now() - t_loop_end).count());
+                    std::chrono::duration<double, std::micro>(t_quiet - t_loop_end).count());
             fprintf(f, "k,record_us,eval_start_us,eval_end_us,consumed_us\n");
             const double base = std::chrono::duration<double>(t_begin.time_since_epoch()).count();
             for (int k = kfirst; k <= *k_end; ++k)

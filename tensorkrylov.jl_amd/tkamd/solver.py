@@ -158,19 +158,30 @@ def _fill_deferred_orthogonality(conv, td, k_last):
     t0 = time.perf_counter()
     part = td.part
     orth = np.zeros(k_last)
+    tm = conv.timing
     if part.nranks > 1:
         # a pending column is written by a flush, whose record all-reduces every rank must
         # join: all ranks flush here, before the one rank's Gram (tk_decomp_gram refuses to
-        # start collectives on a multi-rank handle)
-        td.dev.flush(False)
+        # start collectives on a multi-rank handle) -- when the Gram reads it.  After step
+        # last_j, columns < last_j are in V on every path and column last_j is too unless it
+        # waits in the one-sweep column buffer (even last_j); the decision depends on the step
+        # sequence alone, which every rank shares, so all ranks take the same branch
+        last_j = td.dev.next_step - 1
+        if k_last - 1 >= last_j + (0 if last_j % 2 == 0 else 1):
+            td.dev.flush(False)
+        tm["orth_flush_s"] = time.perf_counter() - t0
     if part.first == 0 and part.nf > 0 and not part.replica:
+        t1 = time.perf_counter()
         G = td.dev.gram(0, k_last)
         orth[:] = orthogonality_losses_from_gram(G)
+        tm["orth_gram_only_s"] = time.perf_counter() - t1
     if part.nranks > 1:
         # (the context's RCCL all-reduce; a backend without a context brings its own)
+        t1 = time.perf_counter()
         orth = (td.ctx if td.ctx is not None else td.dev).allreduce_host(orth)
+        tm["orth_allreduce_s"] = time.perf_counter() - t1
     conv.orthogonality_data[1:k_last] = orth[1:k_last]
-    conv.timing["orth_gram_s"] = time.perf_counter() - t0
+    tm["orth_gram_s"] = time.perf_counter() - t0
 
 
 def _solution(td, k, lam, Ys):

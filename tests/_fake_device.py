@@ -29,6 +29,7 @@ class FakeDecomposition:
         import os
         self.gram_deferred = os.environ.get("TK_FAKE_GRAM_DEFERRED") == "1"
         self.pending = False
+        self.next_step = 0
         self.log = []
 
     def _world(self):
@@ -99,6 +100,7 @@ class FakeDecomposition:
                 self._gram(r, s, j + 1)
             r[s, lay.beta] = f.H[j + 1, j]
         self.pending = True
+        self.next_step = j + 1
         return self._exchange(r)
 
     def flush(self, want=True):
@@ -113,7 +115,12 @@ class FakeDecomposition:
         return self._exchange(np.asarray(x, dtype=np.float64))
 
     def gram(self, f, k, want=True):
-        if self.pending and self._world() > 1:
+        # the ABI's rule (tk_decomp_gram): refused when the product would read the pending
+        # column -- v_{j+1} after step j, or column j itself while it waits in the one-sweep
+        # column buffer (even j, Arnoldi / Lanczos)
+        j = self.next_step - 1
+        in_e = self.method in ("TensorArnoldi", "TensorLanczos") and j % 2 == 0
+        if self.pending and self._world() > 1 and k - 1 >= j + (0 if in_e else 1):
             raise RuntimeError("tk_decomp_gram: column pending; call tk_decomp_flush on every rank first")
         self.log.append("gram")
         V = self.f[self.loc[f]].V[:, :k]

@@ -490,3 +490,43 @@ def test_deferred_orthogonality_after_breakdown(monkeypatch):
     assert len(o) == kb - 1
     assert np.all(o[1:] > 0)
     assert np.array_equal(o[1:], np.asarray(full.orthogonality_data)[1:kb - 1])
+
+
+@pytest.mark.parametrize("cls,sym", [("ConvDiff", False), ("Laplace", True)])
+def test_evaluation_split_over_helpers_is_bitwise_serial(monkeypatch, cls, sym):
+    """The tail iterations' evaluation split into tasks on the solver's helper threads
+    (exp-sum terms, column blocks of Y = Q M, the residual's factors; tkh::ParFor) gives
+    bitwise the single-thread results at every k."""
+    import _fake_device as FD
+    d, n, K = 5, 300, 30
+    rng = np.random.default_rng(5)
+    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    inst = tkamd.SymInstance if sym else tkamd.NonSymInstance
+    A = tkamd.KroneckerMatrix.gallery(inst, d, n, cls)
+    td = tkamd.TensorArnoldi(A, K, backend=FD.backend)
+    td.orthonormalize_first(b)
+    f = FD.FakeDecomposition(td, b)
+    recs = [f.init()] + [f.step(j) for j in range(K)]
+    T = tkamd.compressed.IterationTables(A, K, 1e-9, d)
+    sv = tkamd.compressed.NativeSolver(td.method, d, K, sym, 1.0, T)
+    try:
+        sv.apply(-1, recs[0])
+        for j in range(K):
+            sv.apply(j, recs[j + 1])
+        ks = [k for k in range(2, K + 1) if T.rank[k - 1] >= 1]
+        assert len(ks) > 10
+        out = {}
+        for th in ("1", "3", "4"):
+            monkeypatch.setenv("TKHIP_EVAL_THREADS", th)
+            res = []
+            for k in ks:
+                r = sv.evaluate(k)
+                lam, Y = sv.solution(k)
+                res.append((np.array(r), np.array(lam), np.concatenate([np.ravel(y) for y in Y])))
+            out[th] = res
+        for th in ("3", "4"):
+            for a_, b_ in zip(out["1"], out[th]):
+                for x, y in zip(a_, b_):
+                    assert np.array_equal(x, y, equal_nan=True)
+    finally:
+        sv.close()
