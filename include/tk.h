@@ -335,6 +335,15 @@ tk_status tk_solver_prepare(tk_solver* sv, int nthreads);
  * *k_end may still run; their results are not read. */
 tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, int depth, int nthreads,
                         double* relres, double* projres, double* orth, int* k_end, int* outcome);
+/* orthogonality_loss(V, k) = norm(V[:, 1:k]' V[:, 1:k] - I) for k = 1..K from ONE Gram matrix
+ * G = V[:, 1:K]' V[:, 1:K] (K x K column-major, lower triangle read) into out[K]
+ * (src/orthogonal_bases.jl:250-257, called per iteration at src/tensor_krylov_method.jl:103):
+ * the squared loss grows by column k's diagonal and twice its off-diagonal squares, in the
+ * order tk_solver_evaluate sums a tracked factor's Gram rows.  tk_solver_run fills orth[]
+ * with it on the rank holding factor 1 of a deferred-Gram handle when the Gram launched
+ * behind the last step (tk_decomp_gram_ahead) covers the iterations it ran; entries it
+ * could not fill stay NaN. */
+tk_status tk_orthogonality_losses(int K, const double* G, double* out);
 
 #ifdef __cplusplus
 }

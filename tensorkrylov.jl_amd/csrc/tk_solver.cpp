@@ -358,7 +358,26 @@ static void stop_workers(tk_solver* sv) {
     sv->helpers.reset();
 }
 
+// norm(G[:k, :k] - I), k = 1..K (G column-major, lower triangle): tk_solver_evaluate's sum
+static void orth_losses(int K, const double* G, int ld, double* out) {
+    double acc = 0.0;
+    for (int c = 0; c < K; ++c) {
+        const double dd = G[(size_t)c * ld + c] - 1.0;
+        double off = 0.0;
+        for (int i = 0; i < c; ++i) off += G[(size_t)i * ld + c] * G[(size_t)i * ld + c];
+        acc += dd * dd + 2.0 * off;
+        out[c] = sqrt(acc);
+    }
+}
+
 extern "C" {
+
+tk_status tk_orthogonality_losses(int K, const double* G, double* out) { TK_API_BEGIN
+    if (K < 0 || (K > 0 && (!G || !out))) return tk_fail_internal(TK_ERR_ARG, "tk_orthogonality_losses: bad argument");
+    orth_losses(K, G, K, out);
+    return TK_OK;
+    TK_API_END
+}
 
 tk_status tk_solver_prepare(tk_solver* sv, int nthreads) { TK_API_BEGIN
     if (!sv || nthreads < 1) return tk_fail_internal(TK_ERR_ARG, "tk_solver_prepare: bad argument");
@@ -512,11 +531,23 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     // step (tk_decomp_gram_ahead: no-op on ranks without it), overlapping the host's evaluation
     // of the last iterations; the caller's tk_decomp_gram then only reads it
     bool gram_ahead = false;
+    int gram_k = 0;   // columns of the Gram launched ahead (0: none on this rank)
     auto ahead = [&]() -> tk_status {
         if (gram_ahead || next_issue <= kmax) return TK_OK;
         gram_ahead = true;
-        int kg = 0;
-        return tk_decomp_gram_ahead(dc, &kg);
+        return tk_decomp_gram_ahead(dc, &gram_k);
+    };
+    // ... and once every iteration is dispatched the calling thread reads it (while the
+    // workers evaluate the last iterations) and derives orthogonality_data from it
+    std::vector<double> gram_loss;
+    auto read_gram = [&]() -> tk_status {
+        if (gram_k < 1 || sv->gram_tracked || !gram_loss.empty()) return TK_OK;
+        std::vector<double> G((size_t)gram_k * gram_k);
+        tk_status s2 = tk_decomp_gram(dc, 0, gram_k, G.data());
+        if (s2) return s2;
+        gram_loss.resize(gram_k);
+        orth_losses(gram_k, G.data(), gram_k, gram_loss.data());
+        return TK_OK;
     };
     tk_status st = issue_upto(kfirst + depth - 1);
     if (!st) st = ahead();
@@ -603,6 +634,10 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             lap(t_apply);
         }
         if (err) break;
+        if (k_dispatch > klast) {
+            err = read_gram();
+            if (err) break;
+        }
         Worker& wk = *workers[(k - kfirst) % P];
         wait_done((k - kfirst) % P, k);
         lap(t_wait);
@@ -635,6 +670,8 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     }
     const auto t_loop_end = clk::now();
     if (hp) hp->set_hot(false);
+    if (!err && !gram_loss.empty())
+        for (int k = kfirst; k <= std::min(*k_end, gram_k); ++k) orth[k - 1] = gram_loss[k - 1];
     quiesce();
     const auto t_quiet = clk::now();
     if (etr) {

@@ -223,13 +223,15 @@ def orthogonality_loss_from_gram(G, k):
 def orthogonality_losses_from_gram(G):
     """[norm(V[:,1:k]'V[:,1:k] - I) for k = 1..K] (src/orthogonal_bases.jl:250-257) from one
     Gram matrix G = V[:,1:K]'V[:,1:K] (lower triangle used): the squared loss grows by column
-    k's diagonal and twice its off-diagonal squares, summed in the same order as
-    orthogonality_loss_from_gram's norm would be accumulated up to rounding."""
-    L = np.tril(np.asarray(G, dtype=np.float64))
-    K = L.shape[0]
-    D = L - np.eye(K)
-    row = (D * D).sum(axis=1) * 2.0 - np.diag(D) ** 2    # row k: 2 sum_{i<k} D[k,i]^2 + D[k,k]^2
-    return np.sqrt(np.cumsum(row))
+    k's diagonal and twice its off-diagonal squares (tk_orthogonality_losses -- the sum the
+    native loop applies to the Gram it reads itself, so both give the same bits)."""
+    from . import _lib as L
+    G = np.asarray(G, dtype=np.float64)
+    K = G.shape[0]
+    Gc = np.ascontiguousarray(G.T)          # column-major G: lower triangle (i >= j) at j*K + i
+    out = np.zeros(K)
+    L.check(L.lib().tk_orthogonality_losses(K, L.dptr(Gc), L.dptr(out)))
+    return out
 
 
 # ------------------------------------------------------------------ native iteration driver

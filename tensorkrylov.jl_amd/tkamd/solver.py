@@ -145,13 +145,15 @@ def _gram_deferred(td):
     return bool(getattr(td.dev, "gram_deferred", False))
 
 
-def _fill_deferred_orthogonality(conv, td, k_last):
+def _fill_deferred_orthogonality(conv, td, k_last, native=None):
     """orthogonality_data[k] = orthogonality_loss(V_1, k) (src/tensor_krylov_method.jl:103,
     src/orthogonal_bases.jl:250-257) for k = 2..k_last, from ONE Gram matrix of factor 1's
     basis (tk_decomp_gram: a SYRK on the matrix cores) when the handle does not carry a Gram
     row per step (tk_decomp_gram_deferred).  The values are those the reference computes at
     iteration k: columns 1..k are final once step k is done.  With several ranks the rank
-    owning factor 1 computes them and one all-reduce (every rank calls it here) shares them."""
+    owning factor 1 computes them and one all-reduce (every rank calls it here) shares them.
+    native: orthogonality_data as tk_solver_run left it -- its losses from the Gram launched
+    behind the last step, read during the last evaluations (NaN where it had none)."""
     if not _gram_deferred(td) or k_last < 2:
         return
     from .compressed import orthogonality_losses_from_gram
@@ -172,8 +174,11 @@ def _fill_deferred_orthogonality(conv, td, k_last):
         tm["orth_flush_s"] = time.perf_counter() - t0
     if part.first == 0 and part.nf > 0 and not part.replica:
         t1 = time.perf_counter()
-        G = td.dev.gram(0, k_last)
-        orth[:] = orthogonality_losses_from_gram(G)
+        if native is not None and np.all(np.isfinite(native[1:k_last])):
+            orth[1:] = native[1:k_last]
+        else:
+            G = td.dev.gram(0, k_last)
+            orth[:] = orthogonality_losses_from_gram(G)
         tm["orth_gram_only_s"] = time.perf_counter() - t1
     if part.nranks > 1:
         # (the context's RCCL all-reduce; a backend without a context brings its own)
@@ -235,7 +240,7 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
     if outcome == 1:                                                # :108-118
         lam, Ys = sv.solution(k_end)
         x = _solution(td, k_end, lam, Ys)
-    _fill_deferred_orthogonality(conv, td, k_end)
+    _fill_deferred_orthogonality(conv, td, k_end, conv.orthogonality_data if device and pipelined else None)
     conv.timing["loop_s"] = time.perf_counter() - t_loop
     # the host mirror of H, b~ and factor 1's Gram rows (principal_minors readers)
     H, bt, G = sv.state()

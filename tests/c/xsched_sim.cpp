@@ -129,6 +129,13 @@ tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out) {   // (no collective:
     *k_out = 0;
     return TK_OK;
 }
+tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) {   // (never reached: no Gram ahead)
+    (void)dc;
+    (void)f;
+    (void)k;
+    (void)G;
+    return TK_ERR_STATE;
+}
 
 tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) {
     if (s1 > s0) need_slots(dc, std::min(s1 - 1, dc->jnext));
@@ -184,10 +191,15 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
     tk_solver_destroy(sv);
     if (outcome == 1) flush(&dc);   // basis_mul's flush of the pending column
     // the deferred orthogonality Gram (tkamd.solver._fill_deferred_orthogonality):
-    // every rank flushes, then the rank owning factor 1 runs the Gram, which must start no
-    // collective -- tk_decomp_gram refuses a pending column on a multi-rank handle
-    flush(&dc);
-    if (dc.pending) {
+    // every rank flushes when the Gram of k_end columns reads the pending column -- decided
+    // from the step sequence alone (columns < last_j are written on every path, column last_j
+    // unless it waits in the one-sweep column buffer: even last_j) -- then the rank owning
+    // factor 1 runs the Gram, which must start no collective: tk_decomp_gram refuses a Gram
+    // that reads a pending column on a multi-rank handle
+    const int last_j = dc.jnext - 1;
+    if (k_end - 1 >= last_j + (last_j % 2 == 0 ? 0 : 1)) flush(&dc);
+    const bool in_e = dc.kind == ONESWEEP && last_j % 2 == 0;
+    if (dc.pending && k_end - 1 >= last_j + (in_e ? 0 : 1)) {
         fprintf(stderr, "rank %d: Gram with column %d pending\n", g_rank, dc.jnext);
         exit(4);
     }

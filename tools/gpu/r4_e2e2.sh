@@ -10,7 +10,7 @@ import json; d=json.loads(open('gpurun_out/e2e_$nm.log').read().strip().splitlin
 print('== $nm device', d['value'], 'e2e', e['iterations_s'], 'ratio %.3f' % (e['iterations_s'] / d['value']), 'all', e['iterations_s_all'], 'phases', e['phases_s'])
 print(1e6/d['value'])" > gpurun_out/e2e_$nm.txt
   head -1 gpurun_out/e2e_$nm.txt
-  python3 tools/e2e_trace.py gpurun_out/tr_$nm.csv $(tail -1 gpurun_out/e2e_$nm.txt) | head -3
+  python3 tools/e2e_trace.py gpurun_out/tr_$nm.csv $(tail -1 gpurun_out/e2e_$nm.txt) > gpurun_out/trs_$nm.txt && sed -n 1,3p gpurun_out/trs_$nm.txt
 }
 for rep in a b; do
   for th in 1 3; do
