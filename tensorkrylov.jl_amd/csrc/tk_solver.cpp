@@ -177,11 +177,14 @@ class Helpers : public ParFor {
     unsigned wake_ = 0;
 };
 
-// TKHIP_SOLVER_TAIL_THREADS: tasks (1..4) the last two iterations' evaluations split into
+// TKHIP_SOLVER_TAIL_THREADS: tasks (1..4) the last two iterations' evaluations split into.
+// Default 3 (2 helpers): C4's tail 240-316 -> 115-138 us, end-to-end 0.94 -> 0.96 of the
+// device rate; no change where the host is throughput-bound (C4 emulated N = 8)
+// (profiles/r04/e2e/native_orth_tail_ab.txt, tail_helpers_ab_traced.txt)
 static int tail_threads() {
     static const int v = [] {
         const char* e = getenv("TKHIP_SOLVER_TAIL_THREADS");
-        return e ? std::max(1, std::min(4, atoi(e))) : 1;
+        return e ? std::max(1, std::min(4, atoi(e))) : 3;
     }();
     return v;
 }
