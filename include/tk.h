@@ -247,6 +247,11 @@ int tk_decomp_gram_deferred(tk_decomp* dc);
  * TKHIP_FACTOR_GROUPS=1 at create keeps one stream.  Results are
  * bitwise those of one stream (every kernel is per factor). */
 int tk_decomp_factor_groups(tk_decomp* dc);
+/* 1 when V_s is kept in single-column tiles (the Gram-free one-sweep TensorLanczos: its step
+ * reads one basis column and writes one, 40 bytes per row), 0 for paired columns; a layout
+ * detail every reader of the basis (tk_decomp_get_basis, tk_decomp_basis_mul, tk_decomp_gram)
+ * handles itself.  TKHIP_LANCZOS_SL=0 keeps the pairs. */
+int tk_decomp_single_columns(tk_decomp* dc);
 
 /* basis_tensor_mul! (src/utils.jl:478-488, called at src/tensor_krylov_method.jl:112):
  * X_s = V_s[:, 0..k-1] * Y_s for every local factor, on MFMA (v_mfma_f64_16x16x4).

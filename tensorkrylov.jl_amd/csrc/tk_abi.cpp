@@ -675,6 +675,9 @@ struct tk_decomp {
     // of its basis when asked (tk_decomp_gram) instead of a Gram row per step (TKHIP_GRAM)
     bool gram_deferred = false;
     bool any_gram = false;   // some local factor keeps a per-step Gram row
+    // single-column basis tiles (KArgs::sl): the Gram-free one-sweep TensorLanczos, whose step
+    // reads one column and writes one (TKHIP_LANCZOS_SL=0 keeps the paired columns)
+    bool sl = false;
     double* gram_scr = nullptr;
     bool gram_scr_owned_by_allocs = false;   // (allocated at create: freed with allocs)
     // the Gram values land in host-mapped memory, then a sequence word (k_mirror_records, as
@@ -939,6 +942,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             DA(d.AU, (size_t)dc->ld * sizeof(double));
         }
     }
+    {
+        const char* e = getenv("TKHIP_LANCZOS_SL");
+        dc->sl = method == TK_LANCZOS && dc->onesweep && dc->fin_d && !dc->any_gram && kmax <= ARN_D1_JMAX &&
+                 !(e && e[0] == '0');
+    }
     DA(dc->df, nf * sizeof(DFac));
     {
         hipError_t e = hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice);
@@ -1130,6 +1138,8 @@ int tk_decomp_exchange_signalled(tk_decomp* dc) { return dc && dc->xflag ? 1 : 0
 
 int tk_decomp_next_step(tk_decomp* dc) { return dc ? dc->jnext : -1; }
 
+int tk_decomp_single_columns(tk_decomp* dc) { return dc && dc->sl ? 1 : 0; }
+
 int tk_decomp_matrix_reads(tk_decomp* dc) { return !dc ? -1 : (dc->mfspmv ? 1 : dc->nf); }
 
 int tk_decomp_gram_deferred(tk_decomp* dc) { return dc && dc->gram_deferred ? 1 : 0; }
@@ -1255,6 +1265,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.seq = 0;
     a.ecol = -1;
     a.mfs = 0;
+    a.sl = dc->sl ? 1 : 0;
     return a;
 }
 
@@ -1442,7 +1453,7 @@ static tk_status finalize_pending(tk_decomp* dc, const KArgs& a) {
             // one-sweep Lanczos: v_{j+1} = inv(beta) .* (u_j - alpha v_j) from the step's buffers
             KArgs f = a;
             f.ubuf = (j & 1) ? 0 : 1;
-            f.ecol = (j & 1) ? -1 : j;
+            f.ecol = (dc->sl || (j & 1)) ? -1 : j;   // (single columns: v_j is in V)
             RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, f, 2, s), "fin_d");
         } else if (fd) {
             RUN(TCLS_FIN, 2, launch_fin_d(dc->df, nf, a, 1, s), "fin_d");
@@ -1868,7 +1879,7 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     GJOIN(dc);
     // (one-sweep Arnoldi after an even step: column last_j is still in DFac::E; the flush
     // stores it with the pending column)
-    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && !dc->sl &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     if (dc->pending && nc > 0 && c0 + nc - 1 >= dc->last_j + (in_e ? 0 : 1)) {
         // (as tk_decomp_gram: a one-rank read must not start collectives its peers do not join)
@@ -1888,7 +1899,7 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
     }
     for (int cc = 0; cc < nc; cc += GCH) {
         const int m = std::min(GCH, nc - cc);
-        launch_get_cols(d.V, dc->n, dc->kmax, c0 + cc, m, dc->scratch, s);
+        launch_get_cols(d.V, dc->n, dc->kmax, c0 + cc, m, dc->scratch, dc->sl ? 1 : 0, s);
         LAUNCHCHK("get_cols");
         HIPCHK(hipStreamSynchronize(s));
         HIPCHK(hipMemcpy(out + (size_t)cc * dc->n, dc->scratch, (size_t)dc->n * m * sizeof(double),
@@ -1937,7 +1948,7 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
     }
     dc->ahead_k = 0;   // (this launch's mirror replaces the one launched ahead)
     // every column the product reads must be in V: flush a pending (or column-buffered) one
-    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && !dc->sl &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     if (dc->pending && k - 1 >= dc->last_j + (in_e ? 0 : 1)) {
         // the flush starts record all-reduces (need_slots, the flush slot): with peers, only a
@@ -2010,7 +2021,7 @@ tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out) { TK_API_BEGIN
         !dc->inited || dc->ahead_k > 0)
         return TK_OK;
     // written columns only (no flush: it would start record exchanges on one rank)
-    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep &&
+    const bool in_e = (dc->method == TK_ARNOLDI || dc->method == TK_LANCZOS) && dc->onesweep && !dc->sl &&
                       dc->last_j <= ARN_D1_JMAX && !(dc->last_j & 1);
     int k = dc->pending ? dc->last_j + (in_e ? 0 : 1) : dc->jnext + 1;
     k = std::min(std::min(k, 64), dc->kmax + 1);
@@ -2094,7 +2105,7 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
         KArgs f = a;
         if (dc->onesweep && jl <= ARN_D1_JMAX) {   // as finalize_pending
             f.ubuf = (jl & 1) ? 0 : 1;
-            f.ecol = (jl & 1) ? -1 : jl;
+            f.ecol = (dc->sl || (jl & 1)) ? -1 : jl;
         }
         RUN(TCLS_VY, 1, launch_fin_vy(dc->df, dc->nf, f, dc->Ydev, dc->Xdev, ldy, t, lan1 ? 2 : 0, s), "fin_vy");
         if (lan1) {

@@ -102,6 +102,9 @@ struct KArgs {
     unsigned long long seq;
     int ecol;         // flush of the one-sweep pending column: this column (j) is in DFac::E, not V (-1: none)
     int mfs;          // CGS2 pass 1: A U comes from DFac::AU (k_spmv_mf ran), not from its own gathers
+    int sl;           // 1: V in single-column tiles (column c of a tile at c * 256 doubles, row
+                      // stride 8 B) -- the Gram-free one-sweep TensorLanczos, whose step reads one
+                      // column and writes one; 0: paired columns (tk_kernels.hip header)
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
@@ -180,7 +183,7 @@ enum PostKind {
     POST_SIGNAL = 7      // only mirror the finished record to the host (LanczosReorth)
 };
 void launch_post(const DFac* F, int nf, const KArgs& a, int kind, int flag, int clear, hipStream_t s);
-void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s);
+void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, int sl, hipStream_t s);
 void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int k,
                       int t, hipStream_t s);
 void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s);

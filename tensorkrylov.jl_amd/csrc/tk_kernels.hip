@@ -11,6 +11,11 @@
 // check (num_records = whole column pairs from the tile base) zero-fills the pairs a step
 // does not use; the odd column of a half-used pair is cleared in registers.  All
 // n-length vectors are padded to whole tiles (zeros).
+// The Gram-free one-sweep TensorLanczos (KArgs::sl) keeps the same tiles with SINGLE
+// columns instead, element (r, c) at (r/256)*256*KCP + c*256 + r%256: its step reads one
+// column and writes one, and a pair layout makes that 48 bytes per row instead of 40 (half
+// a pair read for the previous column, the even column's round trip through E).  The
+// readers of a whole basis (V*Y, the Gram, the flush) take both layouts.
 //
 // Numerical scheme (DESIGN.md "Arnoldi step"): the reference's two-pass MGS
 // (src/orthogonal_bases.jl:15-37) is computed as CGS2 -- h1 = V'w, w' = w - V h1,
@@ -86,6 +91,10 @@ __device__ __forceinline__ int64_t vofs(int c, int t) { return ((int64_t)(c >> 1
 __device__ __forceinline__ uint32_t cofs(int c) { return (uint32_t)(c >> 1) * (TPB * 16) + (uint32_t)(c & 1) * 8; }
 __host__ __device__ __forceinline__ int kcp(int kmax) { return (kmax + 2) & ~1; }
 __device__ __forceinline__ uint32_t vrange(int nc) { return (uint32_t)((nc + 1) >> 1) * (TPB * 16); }
+// single-column tiles (KArgs::sl): element offset of (row t, column c), byte offset of column c
+// relative to thread t's base (t*8); vrange covers them too (nc*256*8 <= its pair bytes)
+__device__ __forceinline__ int64_t svofs(int c, int t) { return (int64_t)c * TPB + t; }
+__device__ __forceinline__ uint32_t sofs(int c) { return (uint32_t)c * (TPB * 8); }
 
 // Julia's CSC scatter adds nz*x into y without FMA; keep products and sums separately
 // rounded so the device SpMV equals it bit for bit (__dmul_rn/__dadd_rn are plain
@@ -235,6 +244,14 @@ struct Row {
             last = 2 * p == nc - 1 ? x.x : (2 * p + 1 == nc - 1 ? x.y : last);
         }
         if (nc > MAXC) last = bld(tile, toff + cofs(nc - 1));
+    }
+    // single-column tiles (toff = t*8): columns past nc get an offset beyond the resource
+    __device__ __forceinline__ void load_sl(rsrc_t tile, uint32_t toff, int nc) {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) v[c] = bld(tile, c < nc ? toff + sofs(c) : 0x80000000u);
+        last = nc <= MAXC ? 0.0 : bld(tile, toff + sofs(nc - 1));
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c) last = c == nc - 1 ? v[c] : last;
     }
     // Column c (MAXC - 8 <= c < MAXC, or MAXC == 8; wave-uniform; loaded as zero) := x, and
     // `last` := x.  Masked adds, not a conditional store: that one the compiler merged into
@@ -1373,7 +1390,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 // P1 = [ <u,v_j>, |u|^2, |v_j|^2, <v_j,b>, |wt|^2, <wt,v_j> ] at stride DFac::nwl.  (The
 // reduce stays a launch of its own: ending the step in the factor's last block to arrive
 // took ~1000 same-address agent atomics per factor and measured 10 us slower per step.)
-template <int FMT>
+// SL: single-column tiles -- v_{j-1} is read from its own column and v_j written to its own
+// (40 bytes per row: u, v_{j-1}, b in; v_j, u out); otherwise an even v_j goes to E and the
+// odd step after it stores the pair.
+template <int FMT, bool SL>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lan_1w(const DFac* __restrict__ F, KArgs a,
                                                                                           KArgs b) {
 #pragma clang fp contract(off)
@@ -1408,10 +1428,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         const int64_t r = S + i * TPB + t;
         const bool inb = r >= 0 && r < a.ld;
         const bool ok = r >= 0 && r < a.n;
-        const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * 16) : 0x80000000u;
+        const uint32_t toff = inb ? (uint32_t)((r >> 8) * TS * 8 + (r & 255) * (SL ? 8 : 16)) : 0x80000000u;
         up[i] = inb ? ld(Uin, r) : 0.0;
-        // v_{j-1}: E after an even step, the odd half of its pair otherwise
-        vp[i] = j == 0 ? 0.0 : ((j & 1) ? (inb ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j - 1)));
+        // v_{j-1}: its own column (SL); E after an even step, the odd half of its pair otherwise
+        if (SL) vp[i] = j == 0 ? 0.0 : bld(tv, toff + sofs(j - 1));
+        else vp[i] = j == 0 ? 0.0 : ((j & 1) ? (inb ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j - 1)));
         bv[i] = ok ? ld(d.b, r) : 0.0;
     }
     double vj[LAN_RPT];
@@ -1437,7 +1458,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         }) : 0.0;
         const double u = own ? sub_rn_(av, mul_rn(betap, vp[i])) : 0.0;
         if (own) {
-            if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj[i], vp[i]);
+            if (SL) st(d.V, (r >> 8) * TS + svofs(j, (int)(r & 255)), vj[i]);
+            else if (j & 1) st_pair(d.V, (r >> 8) * TS, j, (int)(r & 255), vj[i], vp[i]);
             else st(d.E, r, vj[i]);
             st(Uout, r, u);
         }
@@ -1483,7 +1505,8 @@ __global__ __launch_bounds__(TPB) void k_init_bd(const DFac* __restrict__ F, KAr
         const double v0 = inv * bv;
         const double* bg = d.b;
         const double av = ok ? spmv<FMT>(d.A, r, [=](int64_t cc) { return mul_rn(inv, ld(bg, cc)); }) : 0.0;
-        st_pair(d.V, (int64_t)tile * TS, 0, threadIdx.x, v0, 0.0);
+        if (a.sl) st(d.V, (int64_t)tile * TS + threadIdx.x, v0);
+        else st_pair(d.V, (int64_t)tile * TS, 0, threadIdx.x, v0, 0.0);
         st(d.U, r, v0);
         const double e[3] = {v0 * bv, v0 * v0, v0 * av};
         reduce_scalars<3>(e, tr, acc, 0, first);
@@ -1499,8 +1522,9 @@ __global__ __launch_bounds__(TPB) void k_init_bd(const DFac* __restrict__ F, KAr
 // MODE 1 (Lanczos TTR): v = (beta == 0 ? 0 : inv(beta) .* W) (src/orthogonal_bases.jl:59);
 //   P1 = [ <v,b> | gram <V[:,c],v> (c<=j) | <v,v> ]  (gram and <v,v>: tracked)  (POST_LAN_FIN)
 // For j + 1 <= 64 columns (the register row); beyond, and for gated launches, the
-// tile-loop kernels above.
-template <int MAXC, int MODE, bool VY = false>
+// tile-loop kernels above.  Single-column tiles (a.sl, MODE 2 only): the Gram-free branch
+// checks a.sl itself; the register-row path (V * Y) takes SL as a template argument.
+template <int MAXC, int MODE, bool VY = false, bool SL = false>
 __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int slot, double* lds,
                                            const double* __restrict__ Yf = nullptr, double* __restrict__ Xf = nullptr,
                                            int ldy = 0, int tq = 0) {
@@ -1522,7 +1546,7 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     const double up2 = MODE == 2 ? ld(a.ubuf ? d.W : d.U, r) : 0.0;
     if (MODE >= 1 && !gram && !VY) {
         // Lanczos without a Gram row: v, the pair store (other half = column j), <v,b>
-        const double vjc = em ? (ok ? ld(d.E, r) : 0.0) : bld(tv, toff + cofs(j));
+        const double vjc = em ? (ok ? ld(d.E, r) : 0.0) : (a.sl ? bld(tv, t * 8u + sofs(j)) : bld(tv, toff + cofs(j)));
         double v;
         if (MODE == 2) {
             v = ok ? mul_rn(inv_beta, sub_rn_(up2, mul_rn(alpha2, vjc))) : 0.0;
@@ -1531,7 +1555,8 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
             v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
         }
         const double other = ((j + 1) & 1) ? vjc : 0.0;
-        st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, other);
+        if (a.sl) st(d.V, (int64_t)slot * TS + svofs(j + 1, t), v);
+        else st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, other);
         double x[16] = {v * ld(d.b, r)};
         acc[t] = rs16(x);
         __syncthreads();
@@ -1547,8 +1572,12 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
     if constexpr (VY)
         for (int i = t; i < tq * ldy; i += TPB) Ys[i] = ld(Yf, i);
     Row<MAXC> R;
-    R.load(tv, toff, em ? j : nc);
-    if (em) R.set_col(j, ok ? ld(d.E, r) : 0.0);
+    if (SL) {
+        R.load_sl(tv, t * 8u, nc);
+    } else {
+        R.load(tv, toff, em ? j : nc);
+        if (em) R.set_col(j, ok ? ld(d.E, r) : 0.0);
+    }
     double v;
     if (MODE == 0) {
         const double up = ld(a.ubuf ? d.W : d.U, r);
@@ -1559,7 +1588,8 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
         const bool zero = ld(d.sc, SC_BETA) == 0.0;
         v = (zero || !ok) ? 0.0 : mul_rn(ld(d.W, r), inv_beta);
     }
-    st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, ((j + 1) & 1) ? R.last : 0.0);
+    if (SL) st(d.V, (int64_t)slot * TS + svofs(j + 1, t), v);
+    else st_pair(d.V, (int64_t)slot * TS, j + 1, t, v, ((j + 1) & 1) ? R.last : 0.0);
     if constexpr (VY) {
         // X_s[r, q] = sum_{c < k} V[r, c] Y_s[c, q] from the register row the flush just
         // loaded (the tile is streamed once for both); Y_s columns zero-padded to ldy >= MAXC
@@ -2396,8 +2426,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 // per 16 x 16 block instead of 14).  Each tail column: every lane accumulates its k-slots'
 // products, the 4 k-slot lanes of a row are summed at the end (xor 16, xor 32; fixed order).
 // The accumulators go through LDS (16 columns at a time) so each X column is written as 256
-// contiguous rows (full lines) instead of 32-B pieces.
-template <int NG, int TL>
+// contiguous rows (full lines) instead of 32-B pieces.  SL: single-column tiles, the two
+// columns of a lane's k-slot pair as two 8-byte loads (16 consecutive rows per k-slot: 128 B).
+template <int NG, int TL, bool SL>
 __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, const double* __restrict__ Y,
                                                double* __restrict__ X, int k, int t, int tile, int t0,
                                                double* Ys) {
@@ -2445,7 +2476,13 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int row = wave * 64 + s * 16 + lr;
-                const d2_t av = bld2(tv, ((uint32_t)(ka >> 1) * TPB + row) * 16u);
+                d2_t av;
+                if (SL) {
+                    av.x = bld(tv, ((uint32_t)ka * TPB + row) * 8u);
+                    av.y = bld(tv, ((uint32_t)(ka + 1) * TPB + row) * 8u);
+                } else {
+                    av = bld2(tv, ((uint32_t)(ka >> 1) * TPB + row) * 16u);
+                }
                 const double a1 = ka + 1 < kn ? av.y : 0.0;   // odd column past k: stale data
 #pragma unroll
                 for (int q = 0; q < NG; ++q)
@@ -2468,8 +2505,13 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int row = wave * 64 + s * 16 + lr;
-                const d2_t av = bld2(tv, ((uint32_t)(kc >> 1) * TPB + row) * 16u);
-                const double x = kc < kn ? ((lk & 1) ? av.y : av.x) : 0.0;
+                double x;
+                if (SL) {
+                    x = kc < kn ? bld(tv, ((uint32_t)kc * TPB + row) * 8u) : 0.0;
+                } else {
+                    const d2_t av = bld2(tv, ((uint32_t)(kc >> 1) * TPB + row) * 16u);
+                    x = kc < kn ? ((lk & 1) ? av.y : av.x) : 0.0;
+                }
 #pragma unroll
                 for (int q = 0; q < NG; ++q)
                     acc[s][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(x, bq[q], acc[s][q], 0, 0, 0);
@@ -2516,20 +2558,20 @@ __device__ __forceinline__ void basis_mul_tile(const DFac& d, const KArgs& a, co
 
 // blockIdx.z = column slice: NG MFMA groups per slice, the last slice of the launch also
 // takes the TL tail columns (slices before it are launched with TL = 0, see launch_basis_mul)
-template <int NG, int TL>
+template <int NG, int TL, bool SL>
 __global__ __launch_bounds__(256) void k_basis_mul(const DFac* __restrict__ F, KArgs a,
                                                    const double* __restrict__ Yall,
                                                    double* __restrict__ Xall, int k, int t, int z0) {
     __shared__ __attribute__((aligned(16))) double Ys[BM_LDS_DOUBLES];
     const int f = blockIdx.y;
-    basis_mul_tile<NG, TL>(F[f], a, Yall + (int64_t)f * k * t, Xall + (int64_t)f * a.ld * t, k, t, blockIdx.x,
+    basis_mul_tile<NG, TL, SL>(F[f], a, Yall + (int64_t)f * k * t, Xall + (int64_t)f * a.ld * t, k, t, blockIdx.x,
                            (z0 + (int)blockIdx.z) * 16 * 2, Ys);
 }
 
 // The pending column's flush (fin_d_tile, MODE 0: Arnoldi) and V * Y of the same tile in one
 // block: the register row the flush loads also feeds the product, so each basis tile is
 // streamed from HBM once for both.  Y: [nf][t][ldy] with zero rows k..ldy-1, k <= j + 1.
-template <int MAXC, int MODE>
+template <int MAXC, int MODE, bool SL>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(MAXC <= TK_VY_OCC4 ? 4 : 3, MAXC <= TK_VY_OCC4 ? 4 : 3)))
 void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Yall, double* __restrict__ Xall,
               int ldy, int t) {
@@ -2538,7 +2580,7 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
     const DFac& d = F[f];
     const int slot = (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3);
     if (slot >= a.ntiles) return;
-    fin_d_tile<MAXC, MODE, true>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
+    fin_d_tile<MAXC, MODE, true, SL>(d, a, slot, lds, Yall + (int64_t)f * t * ldy, Xall + (int64_t)f * a.ld * t, ldy, t);
 }
 
 // ------------------------------------------------------------------ orthogonality Gram on MFMA
@@ -2566,7 +2608,8 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
 #ifndef TK_GRAM_GQ
 #define TK_GRAM_GQ 8   // row quads whose loads are in flight before their MFMAs
 #endif
-template <int NC16, int TAIL>
+// SL: single-column tiles (the pair of group 0/1 and the tail pairs as two 8-byte loads).
+template <int NC16, int TAIL, bool SL>
 __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs a, int f, int k,
                                               double* __restrict__ Pg) {
     constexpr int NGR = 2 + NC16;
@@ -2607,11 +2650,23 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
 #pragma unroll
             for (int q = 0; q < GQ; ++q) {
                 const uint32_t row = (uint32_t)(gq + (q0 + q) * 4);
-                x[q] = bld2(tv, ((uint32_t)ci * TPB + row) * 16u);
+                if (SL) {
+                    x[q].x = bld(tv, ((uint32_t)(2 * ci) * TPB + row) * 8u);
+                    x[q].y = bld(tv, ((uint32_t)(2 * ci + 1) * TPB + row) * 8u);
 #pragma unroll
-                for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, cofs(32 + 16 * g + ci) + row * 16u);
+                    for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, sofs(32 + 16 * g + ci) + row * 8u);
 #pragma unroll
-                for (int p = 0; p < NTP; ++p) tl[q][p] = bld2(tv, ((uint32_t)(K0 / 2 + p) * TPB + row) * 16u);
+                    for (int p = 0; p < NTP; ++p) {
+                        tl[q][p].x = bld(tv, ((uint32_t)(K0 + 2 * p) * TPB + row) * 8u);
+                        tl[q][p].y = bld(tv, ((uint32_t)(K0 + 2 * p + 1) * TPB + row) * 8u);
+                    }
+                } else {
+                    x[q] = bld2(tv, ((uint32_t)ci * TPB + row) * 16u);
+#pragma unroll
+                    for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, cofs(32 + 16 * g + ci) + row * 16u);
+#pragma unroll
+                    for (int p = 0; p < NTP; ++p) tl[q][p] = bld2(tv, ((uint32_t)(K0 / 2 + p) * TPB + row) * 16u);
+                }
             }
 #pragma unroll
             for (int q = 0; q < GQ; ++q) {
@@ -2715,11 +2770,12 @@ __global__ __launch_bounds__(TPB) void k_spmv(SpM A, const double* __restrict__ 
 // ------------------------------------------------------------------ tile-major gather/scatter
 // out[c*n + r] = V[r, c0 + c] for one factor (column extraction for the ABI)
 __global__ __launch_bounds__(TPB) void k_get_cols(const double* __restrict__ V, int64_t n, int kmax,
-                                                  int c0, int nc, double* __restrict__ out) {
+                                                  int c0, int nc, double* __restrict__ out, int sl) {
     const int64_t TS = (int64_t)TPB * kcp(kmax);
     const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
     const int c = blockIdx.y;
-    if (r < n && c < nc) st(out, (int64_t)c * n + r, ld(V, (r >> 8) * TS + vofs(c0 + c, (int)(r & 255))));
+    const int64_t o = sl ? svofs(c0 + c, (int)(r & 255)) : vofs(c0 + c, (int)(r & 255));
+    if (r < n && c < nc) st(out, (int64_t)c * n + r, ld(V, (r >> 8) * TS + o));
 }
 
 // ------------------------------------------------------------------ launchers
@@ -2853,7 +2909,8 @@ void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     const dim3 grid((npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0), nf);
     with_band_fmt(a.fmt, [&](auto FM) {
-        hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
+        if (a.sl) hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value, true>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
+        else hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value, false>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
     });
 }
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, hipStream_t s) {
@@ -2921,8 +2978,9 @@ void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, doubl
     const size_t lds = ((size_t)((M + 15) / 16 + 1) * TPB + (size_t)t * ldy) * sizeof(double);   // acc + Y_s
     const dim3 grid((a.ntiles + 7) / 8 * 8, nf);
     with_maxc(nc, [&](auto Mc) {
-        if (mode == 2) hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 2>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
-        else hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 0>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
+        if (mode == 2 && a.sl) hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 2, true>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
+        else if (mode == 2) hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 2, false>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
+        else hipLaunchKernelGGL((k_fin_vy<decltype(Mc)::value, 0, false>), grid, dim3(TPB), lds, s, F, a, Y, X, ldy, t);
     });
 }
 void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
@@ -2980,11 +3038,15 @@ void launch_basis_mul(const DFac* F, int nf, const KArgs& a, const double* Y, do
     }
     const int nz = ng > 2 ? (ng - 1) / 2 : 0;   // full slices of two groups before the last
     const int ngl = ng - 2 * nz;                // groups of the last slice (0, 1 or 2)
-    if (nz > 0)
-        hipLaunchKernelGGL((k_basis_mul<2, 0>), dim3(a.ntiles, nf, nz), dim3(256), 0, s, F, a, Y, X, k, t, 0);
+    if (nz > 0 && a.sl)
+        hipLaunchKernelGGL((k_basis_mul<2, 0, true>), dim3(a.ntiles, nf, nz), dim3(256), 0, s, F, a, Y, X, k, t, 0);
+    else if (nz > 0)
+        hipLaunchKernelGGL((k_basis_mul<2, 0, false>), dim3(a.ntiles, nf, nz), dim3(256), 0, s, F, a, Y, X, k, t, 0);
 #define TK_BM_CASE(G_, L_)                                                                             \
-    if (ngl == G_ && tl == L_)                                                                        \
-        hipLaunchKernelGGL((k_basis_mul<G_, L_>), dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t, nz);
+    if (ngl == G_ && tl == L_ && a.sl)                                                                \
+        hipLaunchKernelGGL((k_basis_mul<G_, L_, true>), dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t, nz); \
+    else if (ngl == G_ && tl == L_)                                                                   \
+        hipLaunchKernelGGL((k_basis_mul<G_, L_, false>), dim3(a.ntiles, nf, 1), dim3(256), 0, s, F, a, Y, X, k, t, nz);
     TK_BM_CASE(0, 1) TK_BM_CASE(0, 2) TK_BM_CASE(0, 3) TK_BM_CASE(0, 4)
     TK_BM_CASE(1, 0) TK_BM_CASE(1, 1) TK_BM_CASE(1, 2) TK_BM_CASE(1, 3) TK_BM_CASE(1, 4)
     TK_BM_CASE(2, 0) TK_BM_CASE(2, 1) TK_BM_CASE(2, 2) TK_BM_CASE(2, 3) TK_BM_CASE(2, 4)
@@ -3044,7 +3106,8 @@ void launch_gram(const DFac* F, int f, const KArgs& a, int k, double* scratch, h
     int nc16, tail;
     gram_config(k, nc16, tail);
 #define TK_GRAM_CASE(A_, B_)                                                                       \
-    if (nc16 == A_ && tail == B_) hipLaunchKernelGGL((k_gram<A_, B_>), dim3(nb), dim3(256), 0, s, F, a, f, k, P);
+    if (nc16 == A_ && tail == B_ && a.sl) hipLaunchKernelGGL((k_gram<A_, B_, true>), dim3(nb), dim3(256), 0, s, F, a, f, k, P); \
+    else if (nc16 == A_ && tail == B_) hipLaunchKernelGGL((k_gram<A_, B_, false>), dim3(nb), dim3(256), 0, s, F, a, f, k, P);
     TK_GRAM_CASE(0, 0) TK_GRAM_CASE(0, 1) TK_GRAM_CASE(0, 2) TK_GRAM_CASE(0, 3) TK_GRAM_CASE(0, 4)
     TK_GRAM_CASE(1, 0) TK_GRAM_CASE(1, 1) TK_GRAM_CASE(1, 2) TK_GRAM_CASE(1, 3) TK_GRAM_CASE(1, 4)
     TK_GRAM_CASE(2, 0)
@@ -3060,9 +3123,9 @@ void launch_spmv(const SpM& A, const double* x, double* y, hipStream_t s) {
         hipLaunchKernelGGL((k_spmv<decltype(FM)::value>), dim3(nb), dim3(TPB), 0, s, A, x, y);
     });
 }
-void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, hipStream_t s) {
+void launch_get_cols(const double* V, int64_t n, int kmax, int c0, int nc, double* out, int sl, hipStream_t s) {
     const int nb = (int)((n + TPB - 1) / TPB);
-    hipLaunchKernelGGL(k_get_cols, dim3(nb, nc), dim3(TPB), 0, s, V, n, kmax, c0, nc, out);
+    hipLaunchKernelGGL(k_get_cols, dim3(nb, nc), dim3(TPB), 0, s, V, n, kmax, c0, nc, out, sl);
 }
 
 }  // namespace tk

@@ -63,6 +63,7 @@ def lib():
         "tk_decomp_matrix_reads": (I, [P]),
         "tk_decomp_gram_deferred": (I, [P]),
         "tk_decomp_factor_groups": (I, [P]),
+        "tk_decomp_single_columns": (I, [P]),
         "tk_decomp_gram": (I, [P, I, I, DP]),
         "tk_decomp_gram_ahead": (I, [P, ctypes.POINTER(I)]),
         "tk_decomp_init": (I, [P, DP]),
@@ -102,7 +103,7 @@ EXPORTS = ("tk_last_error", "tk_version", "tk_ctx_create", "tk_ctx_destroy", "tk
            "tk_matrix_from_csc", "tk_matrix_from_csr", "tk_matrix_destroy", "tk_matrix_format", "tk_matvec",
            "tk_record_len", "tk_decomp_create", "tk_decomp_destroy", "tk_decomp_arnoldi_sweeps",
            "tk_decomp_exchange_signalled", "tk_decomp_set_replica", "tk_decomp_agree", "tk_decomp_next_step",
-           "tk_decomp_matrix_reads", "tk_decomp_gram_deferred", "tk_decomp_factor_groups", "tk_decomp_gram", "tk_decomp_gram_ahead",
+           "tk_decomp_matrix_reads", "tk_decomp_gram_deferred", "tk_decomp_factor_groups", "tk_decomp_single_columns", "tk_decomp_gram", "tk_decomp_gram_ahead",
            "tk_decomp_init",
            "tk_decomp_step", "tk_decomp_sweep", "tk_decomp_flush", "tk_decomp_records",
            "tk_decomp_get_basis", "tk_decomp_basis_mul", "tk_timing_enable", "tk_timing_read",

@@ -159,6 +159,12 @@ class DeviceDecomposition:
         return int(self.ctx._lib.tk_decomp_factor_groups(self.h))
 
     @property
+    def single_columns(self):
+        """V_s in single-column tiles (tk_decomp_single_columns): the Gram-free one-sweep
+        TensorLanczos; paired columns otherwise."""
+        return bool(self.ctx._lib.tk_decomp_single_columns(self.h))
+
+    @property
     def gram_deferred(self):
         """Factor 0's Gram comes from one SYRK (gram()) rather than per-step record rows
         (tk_decomp_gram_deferred)."""

@@ -152,3 +152,53 @@ def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
             assert np.array_equal(x, y)
         for x, y in zip(aX, bX):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("d,K", [(2, 40), (3, 41)])
+def test_lanczos_single_column_layout_bitwise_equal_pairs(ctx, d, K, monkeypatch):
+    """The Gram-free one-sweep TensorLanczos keeps V_s in single-column tiles (its step reads
+    v_{j-1} and writes v_j: 40 bytes per row instead of 48).  Every reader of the basis takes
+    the layout: records (step by step, as a sweep), the columns read back before and after the
+    flush, factor 1's Gram (MFMA SYRK), the fused flush + V*Y and the MFMA V*Y with a VALU tail
+    are bitwise those of the paired-column layout (TKHIP_LANCZOS_SL=0), odd and even K."""
+    import tkamd as tk
+    monkeypatch.delenv("TKHIP_GRAM", raising=False)
+    monkeypatch.delenv("TKHIP_LANCZOS_GROUPS", raising=False)
+    n = 3000
+    rng = np.random.default_rng(79)
+    mat = tk.assemble_matrix(n, "Laplace")
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+    Y1 = [rng.standard_normal((K, 5)) for _ in range(d)]
+    Y2 = [rng.standard_normal((K + 1, 17)) for _ in range(d)]
+    out = {}
+    for sl in ("0", "1"):
+        monkeypatch.setenv("TKHIP_LANCZOS_SL", sl)
+        A = tk.DeviceMatrix(ctx, mat)
+        dev = tk.DeviceDecomposition(ctx, tk._lib.TK_LANCZOS, d, 0, [A] * d, bs, K)
+        assert dev.arnoldi_sweeps == 1 and dev.gram_deferred
+        assert dev.single_columns == (sl == "1")
+        r0 = dev.init()
+        recs = [dev.step(j) for j in range(9)]
+        for j in range(9, 17):
+            dev.step_async(j)
+        recs.append(dev.records(10, 17))
+        dev.sweep(17, K)
+        recs.append(dev.records(0, K + 1))
+        G = dev.gram(0, K - 1)                         # written columns only
+        V0 = [dev.basis(f, 0, K - 1) for f in range(d)]
+        X1 = dev.basis_mul(K, Y1)                      # pending column: the fused flush + V*Y
+        recs.append(dev.records(K + 1, K + 2))
+        X2 = dev.basis_mul(K + 1, Y2)                  # flushed: k_basis_mul (MFMA + VALU tail)
+        V1 = [dev.basis(f, 0, K + 1) for f in range(d)]
+        G1 = dev.gram(0, K + 1)
+        out[sl] = (r0, recs, G, V0, X1, X2, V1, G1)
+        dev.close()
+        A.close()
+    a, b = out["0"], out["1"]
+    assert np.array_equal(a[0], b[0])
+    for x, y in zip(a[1], b[1]):
+        assert np.array_equal(x, y)
+    for i in range(2, 8):
+        xs, ys = (a[i], b[i]) if isinstance(a[i], list) else ([a[i]], [b[i]])
+        for x, y in zip(xs, ys):
+            assert np.array_equal(x, y)
