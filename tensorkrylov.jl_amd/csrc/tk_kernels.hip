@@ -2608,7 +2608,8 @@ void k_fin_vy(const DFac* __restrict__ F, KArgs a, const double* __restrict__ Ya
 #ifndef TK_GRAM_GQ
 #define TK_GRAM_GQ 8   // row quads whose loads are in flight before their MFMAs
 #endif
-// SL: single-column tiles (the pair of group 0/1 and the tail pairs as two 8-byte loads).
+// SL: single-column tiles -- two consecutive rows of a column per lane and dwordx4, two MFMA
+// rounds per load (a different row-to-slot assignment: the same sums in another order).
 template <int NC16, int TAIL, bool SL>
 __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs a, int f, int k,
                                               double* __restrict__ Pg) {
@@ -2635,13 +2636,67 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
 #pragma unroll
     for (int g = 0; g < NC16; ++g) cm[g] = 32 + 16 * g + ci < k;
     const int gq = w * 64 + kr;   // row of quad 0 of this lane
+    // the products of one row slot: v[NGR] = this lane's entries of the column groups, tt[TA]
+    // = the tail columns of its row
+#define TK_GRAM_ACC(v, tt)                                                                               \
+    {                                                                                                   \
+        int i_ = 0;                                                                                     \
+        _Pragma("unroll") for (int ga = 0; ga < NGR; ++ga)                                              \
+            _Pragma("unroll") for (int gb = ga; gb < NGR; ++gb, ++i_)                                   \
+                acc[i_] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i_], 0, 0, 0);        \
+        if (TAIL > 0) {                                                                                 \
+            double own = 0.0; /* tail column ci of this row (lanes ci < TAIL) */                        \
+            _Pragma("unroll") for (int x2 = 0; x2 < TA; ++x2) own = ci == x2 ? tt[x2] : own;            \
+            _Pragma("unroll") for (int x2 = 0; x2 < TA; ++x2) {                                         \
+                _Pragma("unroll") for (int s = 0; s < NGR; ++s) tac[x2][s] = fma(tt[x2], v[s], tac[x2][s]); \
+                tac[x2][NGR] = fma(tt[x2], own, tac[x2][NGR]);                                          \
+            }                                                                                           \
+        }                                                                                               \
+    }
     // (loads of the next batch issued before this batch's MFMAs -- ping-pong buffers -- measured
     // 8-20 % slower: the register budget drops the launch to fewer waves)
     for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
         const rsrc_t tv = mkrsrc(d.V + (int64_t)tile * TS, vrange(k));
+        constexpr int GQ = TK_GRAM_GQ;
+        if constexpr (SL) {
+            // single-column tiles: each lane loads TWO consecutive rows of a column per dwordx4
+            // (the 4 row slots of a load then cover 8 rows: 64-byte runs per column, as the
+            // pairs), feeding two MFMA rounds (.x rows, then .y rows) -- the sum over rows is
+            // order-free.  GQ/2 such octets in flight.
+            constexpr int GO = GQ >= 2 ? GQ / 2 : 1;
+#pragma unroll 1
+            for (int o0 = 0; o0 < 8; o0 += GO) {
+                d2_t xe[GO], xo[GO];
+                d2_t y2[GO][NC16 > 0 ? NC16 : 1];
+                d2_t tc[GO][TA];
+#pragma unroll
+                for (int o = 0; o < GO; ++o) {
+                    const uint32_t row = (uint32_t)(w * 64 + 8 * (o0 + o) + 2 * kr);
+                    xe[o] = bld2(tv, ((uint32_t)(2 * ci) * TPB + row) * 8u);
+                    xo[o] = bld2(tv, ((uint32_t)(2 * ci + 1) * TPB + row) * 8u);
+#pragma unroll
+                    for (int g = 0; g < NC16; ++g) y2[o][g] = bld2(tv, sofs(32 + 16 * g + ci) + row * 8u);
+#pragma unroll
+                    for (int x2 = 0; x2 < TAIL; ++x2) tc[o][x2] = bld2(tv, ((uint32_t)(K0 + x2) * TPB + row) * 8u);
+                }
+#pragma unroll
+                for (int o = 0; o < GO; ++o)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        double v[NGR], tt[TA];
+                        v[0] = ev ? (h ? xe[o].y : xe[o].x) : 0.0;
+                        v[1] = od ? (h ? xo[o].y : xo[o].x) : 0.0;
+#pragma unroll
+                        for (int g = 0; g < NC16; ++g) v[2 + g] = cm[g] ? (h ? y2[o][g].y : y2[o][g].x) : 0.0;
+#pragma unroll
+                        for (int x2 = 0; x2 < TA; ++x2) tt[x2] = TAIL > 0 ? (h ? tc[o][x2].y : tc[o][x2].x) : 0.0;
+                        TK_GRAM_ACC(v, tt)
+                    }
+            }
+            continue;
+        }
         // GQ row quads' loads in flight before their MFMAs (pairs past k read 0; the odd
         // column k of the last pair is stale and masked)
-        constexpr int GQ = TK_GRAM_GQ;
 #pragma unroll 1
         for (int q0 = 0; q0 < 16; q0 += GQ) {
             d2_t x[GQ];
@@ -2650,54 +2705,26 @@ __global__ __launch_bounds__(256) void k_gram(const DFac* __restrict__ F, KArgs 
 #pragma unroll
             for (int q = 0; q < GQ; ++q) {
                 const uint32_t row = (uint32_t)(gq + (q0 + q) * 4);
-                if (SL) {
-                    x[q].x = bld(tv, ((uint32_t)(2 * ci) * TPB + row) * 8u);
-                    x[q].y = bld(tv, ((uint32_t)(2 * ci + 1) * TPB + row) * 8u);
+                x[q] = bld2(tv, ((uint32_t)ci * TPB + row) * 16u);
 #pragma unroll
-                    for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, sofs(32 + 16 * g + ci) + row * 8u);
+                for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, cofs(32 + 16 * g + ci) + row * 16u);
 #pragma unroll
-                    for (int p = 0; p < NTP; ++p) {
-                        tl[q][p].x = bld(tv, ((uint32_t)(K0 + 2 * p) * TPB + row) * 8u);
-                        tl[q][p].y = bld(tv, ((uint32_t)(K0 + 2 * p + 1) * TPB + row) * 8u);
-                    }
-                } else {
-                    x[q] = bld2(tv, ((uint32_t)ci * TPB + row) * 16u);
-#pragma unroll
-                    for (int g = 0; g < NC16; ++g) y[q][g] = bld(tv, cofs(32 + 16 * g + ci) + row * 16u);
-#pragma unroll
-                    for (int p = 0; p < NTP; ++p) tl[q][p] = bld2(tv, ((uint32_t)(K0 / 2 + p) * TPB + row) * 16u);
-                }
+                for (int p = 0; p < NTP; ++p) tl[q][p] = bld2(tv, ((uint32_t)(K0 / 2 + p) * TPB + row) * 16u);
             }
 #pragma unroll
             for (int q = 0; q < GQ; ++q) {
-                double v[NGR];
+                double v[NGR], tt[TA];
                 v[0] = ev ? x[q].x : 0.0;
                 v[1] = od ? x[q].y : 0.0;
 #pragma unroll
                 for (int g = 0; g < NC16; ++g) v[2 + g] = cm[g] ? y[q][g] : 0.0;
-                int i = 0;
 #pragma unroll
-                for (int ga = 0; ga < NGR; ++ga)
-#pragma unroll
-                    for (int gb = ga; gb < NGR; ++gb, ++i)
-                        acc[i] = __builtin_amdgcn_mfma_f64_16x16x4f64(v[ga], v[gb], acc[i], 0, 0, 0);
-                if (TAIL > 0) {
-                    double tt[TA];
-#pragma unroll
-                    for (int x2 = 0; x2 < TA; ++x2) tt[x2] = (x2 & 1) ? tl[q][x2 >> 1].y : tl[q][x2 >> 1].x;
-                    double own = 0.0;   // tail column ci of this row (lanes ci < TAIL)
-#pragma unroll
-                    for (int x2 = 0; x2 < TA; ++x2) own = ci == x2 ? tt[x2] : own;
-#pragma unroll
-                    for (int x2 = 0; x2 < TA; ++x2) {
-#pragma unroll
-                        for (int s = 0; s < NGR; ++s) tac[x2][s] = fma(tt[x2], v[s], tac[x2][s]);
-                        tac[x2][NGR] = fma(tt[x2], own, tac[x2][NGR]);
-                    }
-                }
+                for (int x2 = 0; x2 < TA; ++x2) tt[x2] = TAIL > 0 ? ((x2 & 1) ? tl[q][x2 >> 1].y : tl[q][x2 >> 1].x) : 0.0;
+                TK_GRAM_ACC(v, tt)
             }
         }
     }
+#undef TK_GRAM_ACC
     // waves 0, 1, 2, 3 summed in this order
     for (int ww = 0; ww < 4; ++ww) {
         if (w == ww) {

@@ -159,8 +159,9 @@ def test_lanczos_single_column_layout_bitwise_equal_pairs(ctx, d, K, monkeypatch
     """The Gram-free one-sweep TensorLanczos keeps V_s in single-column tiles (its step reads
     v_{j-1} and writes v_j: 40 bytes per row instead of 48).  Every reader of the basis takes
     the layout: records (step by step, as a sweep), the columns read back before and after the
-    flush, factor 1's Gram (MFMA SYRK), the fused flush + V*Y and the MFMA V*Y with a VALU tail
-    are bitwise those of the paired-column layout (TKHIP_LANCZOS_SL=0), odd and even K."""
+    flush, the fused flush + V*Y and the MFMA V*Y with a VALU tail are bitwise those of the
+    paired-column layout (TKHIP_LANCZOS_SL=0), odd and even K; factor 1's Gram (MFMA SYRK,
+    two rows per lane and load in single columns: its row sums in another order) to 1e-13."""
     import tkamd as tk
     monkeypatch.delenv("TKHIP_GRAM", raising=False)
     monkeypatch.delenv("TKHIP_LANCZOS_GROUPS", raising=False)
@@ -198,7 +199,10 @@ def test_lanczos_single_column_layout_bitwise_equal_pairs(ctx, d, K, monkeypatch
     assert np.array_equal(a[0], b[0])
     for x, y in zip(a[1], b[1]):
         assert np.array_equal(x, y)
-    for i in range(2, 8):
-        xs, ys = (a[i], b[i]) if isinstance(a[i], list) else ([a[i]], [b[i]])
-        for x, y in zip(xs, ys):
+    for i in (3, 4, 5, 6):
+        for x, y in zip(a[i], b[i]):
             assert np.array_equal(x, y)
+    for i in (2, 7):
+        assert a[i].shape == b[i].shape
+        assert np.abs(a[i] - b[i]).max() <= 1e-13
+        assert np.abs(np.diag(b[i]) - 1.0).max() < 1e-8
