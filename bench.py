@@ -333,8 +333,11 @@ def main():
     out = None
     if rank == 0:
         traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (args.config, world))
-        if os.path.exists(pmc_path) and not args.emulate_ranks and method == CONFIGS[args.config][3]:
+        # PMC HBM bytes per step of this config and method (tools/pmc_traffic.py; the config's
+        # own method: pmc_<config>_n<N>.json, another: pmc_<config>_<method>_n<N>.json)
+        tag = args.config if method == CONFIGS[args.config][3] else "%s_%s" % (args.config, method)
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_%s_n%d.json" % (tag, world))
+        if os.path.exists(pmc_path) and not args.emulate_ranks:
             try:
                 traffic = json.load(open(pmc_path)).get("hbm_bytes_per_step")
             except Exception:

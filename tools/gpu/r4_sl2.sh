@@ -12,6 +12,6 @@ rm -rf $R/gpurun_out/pmcl_fetch $R/gpurun_out/pmcl_write
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmcl_fetch -o run -- python3 $R/bench.py --method TensorLanczos --pmc-mode > $R/gpurun_out/pmcl_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmcl_write -o run -- python3 $R/bench.py --method TensorLanczos --pmc-mode > $R/gpurun_out/pmcl_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
 cd $R
-python3 tools/pmc_traffic.py gpurun_out/pmcl_fetch gpurun_out/pmcl_write C2 1 50 gpurun_out/pmc_C2_lanczos_n1.json
+python3 tools/pmc_traffic.py gpurun_out/pmcl_fetch gpurun_out/pmcl_write C2 1 50 gpurun_out/pmc_C2_TensorLanczos_n1.json
 python3 tools/pmc_kernels.py gpurun_out/pmcl_fetch/run_counter_collection.csv --match k_lan_1w
 python3 tools/pmc_kernels.py gpurun_out/pmcl_write/run_counter_collection.csv --match k_lan_1w
