@@ -315,6 +315,13 @@ __device__ __forceinline__ void st_pair(double* V, int64_t tile_base, int c, int
 #ifndef TK_WT
 #define TK_WT 1
 #endif
+// k_reduce256's hand-off of the reduced values to the block that evaluates the next step's
+// scalars: 0 = agent-scope relaxed atomics with the store's completion awaited before the
+// arrival add (measured correct on gfx950), 1 = a release/acquire add + acquire fence (the
+// HIP memory model's own guarantee)
+#ifndef TK_RED_MM
+#define TK_RED_MM 0
+#endif
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_wt(double* p, int64_t i, double v) {
 #if TK_WT
@@ -2009,8 +2016,13 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             // on this 8-XCD part: 5x slower pass kernels when tried.  ctr's reset
             // below is ordered before the next launch by the kernel boundary.
             __hip_atomic_store(d.RED1 + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if TK_RED_MM
+            // memory-model form: the add releases this block's value and acquires the others'
+            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
+#else
             __builtin_amdgcn_s_waitcnt(0);
             last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
+#endif
         }
     }
     if (coefJ < 0 && coefJ != RED_LAN) return;
@@ -2019,6 +2031,10 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     const double al_est = coefJ == RED_LAN ? ld(d.sc, SC_ALPHA) : 0.0;
     __syncthreads();
     if (!last) return;
+#if TK_RED_MM
+    // (every wave of the last block: its loads ordered after thread 0's acquire)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
     auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     if (coefJ == RED_LAN) {
         lan_step_record(d, ax, (int)blockIdx.y, cld(0), cld(2), cld(3), cld(4), cld(5), al_est,
