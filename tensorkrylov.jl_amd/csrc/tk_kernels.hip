@@ -2012,9 +2012,10 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             // table in /opt/skills/guides/MI355X_MICROARCH.md (stores and loads sc1 = the
             // agent-scope relaxed atomics here, vmcnt(0) before the add): measured correct on
             // gfx950, not an architectural guarantee.  The memory-model form -- a
-            // release on the add, an acquire in the last block -- writes back / invalidates L2
-            // on this 8-XCD part: 5x slower pass kernels when tried.  ctr's reset
-            // below is ordered before the next launch by the kernel boundary.
+            // release on the add, an acquire in the last block (TK_RED_MM=1) -- writes back /
+            // invalidates L2 on this 8-XCD part: C2 -5 %, C1 -12 %
+            // (profiles/r04/reduce_handoff_mm_ab.txt).  ctr's reset below is ordered before the
+            // next launch by the kernel boundary.
             __hip_atomic_store(d.RED1 + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #if TK_RED_MM
             // memory-model form: the add releases this block's value and acquires the others'
