@@ -568,6 +568,12 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     // bitwise the same), which spin from the dispatch of iteration klast-2 on
     Helpers* hp = sv->helpers.get();
     const int tail = hp ? tail_threads() : 1;
+    struct HotOff {   // (the helpers stop spinning on every way out of the loop, exceptions too)
+        Helpers* h;
+        ~HotOff() {
+            if (h) h->set_hot(false);
+        }
+    } hot_off{hp};
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
