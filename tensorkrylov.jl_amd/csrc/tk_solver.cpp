@@ -189,6 +189,15 @@ static int tail_threads() {
     return v;
 }
 
+// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers
+static int tail_iters() {
+    static const int v = [] {
+        const char* e = getenv("TKHIP_SOLVER_TAIL_ITERS");
+        return e ? std::max(1, std::min(64, atoi(e))) : 2;
+    }();
+    return v;
+}
+
 }  // namespace
 
 struct tk_solver {
@@ -579,10 +588,10 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             std::lock_guard<std::mutex> lk(pool.mu);
             pool.done[w] = 0;
         }
-        if (hp && k >= klast - 2) hp->set_hot(true);
+        if (hp && k >= klast - tail_iters()) hp->set_hot(true);
         {
             std::lock_guard<std::mutex> lk(workers[w]->mu);
-            workers[w]->ws.nthreads = k >= klast - 1 ? tail : 1;
+            workers[w]->ws.nthreads = k > klast - tail_iters() ? tail : 1;
             workers[w]->ws.par = hp;
             workers[w]->job = k;
         }
