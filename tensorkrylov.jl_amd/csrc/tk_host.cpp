@@ -17,6 +17,7 @@
 // (tests/test_host.py).
 #include <immintrin.h>
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -404,8 +405,81 @@ static inline double dot4(int n, const double* a, const double* b) {
 // of 8 rows x 4 columns (eight ymm accumulators; each k step two A loads, four broadcasts,
 // eight FMAs), then 4-row and single-row / single-column edges.  Every C entry is one
 // accumulation in k order (a fused multiply-add per term), whatever block it falls in.
+// The same products with zmm registers (AVX-512F, both the box's EPYC 9575F and this image's
+// build host have it): blocks of 16 rows x 4 columns, the row edge through masked loads and
+// stores.  Each C entry is the same k-ordered chain of fused multiply-adds as in the AVX2
+// kernel, so the two give the same bits (TKHIP_HOST_AVX512=0 selects the AVX2 kernel).
+__attribute__((target("avx512f"))) static void gemm_nn_512(int m, int n, int kk, const double* __restrict A, int lda,
+                                                           const double* __restrict B, int ldb, double* __restrict C,
+                                                           int ldc) {
+    int j0 = 0;
+    for (; j0 + 4 <= n; j0 += 4) {
+        const double* b0 = B + (size_t)j0 * ldb;
+        const double* b1 = b0 + ldb;
+        const double* b2 = b1 + ldb;
+        const double* b3 = b2 + ldb;
+        for (int i0 = 0; i0 < m; i0 += 16) {
+            const int r = m - i0;
+            const __mmask8 k0 = (__mmask8)(r >= 8 ? 0xFF : (1u << r) - 1u);
+            const __mmask8 k1 = (__mmask8)(r >= 16 ? 0xFF : (r > 8 ? (1u << (r - 8)) - 1u : 0u));
+            __m512d c00 = _mm512_setzero_pd(), c01 = _mm512_setzero_pd(), c10 = _mm512_setzero_pd(),
+                    c11 = _mm512_setzero_pd(), c20 = _mm512_setzero_pd(), c21 = _mm512_setzero_pd(),
+                    c30 = _mm512_setzero_pd(), c31 = _mm512_setzero_pd();
+            for (int c = 0; c < kk; ++c) {
+                const double* a = A + (size_t)c * lda + i0;
+                const __m512d a0 = _mm512_maskz_loadu_pd(k0, a), a1 = _mm512_maskz_loadu_pd(k1, a + 8);
+                __m512d bv = _mm512_set1_pd(b0[c]);
+                c00 = _mm512_fmadd_pd(a0, bv, c00);
+                c01 = _mm512_fmadd_pd(a1, bv, c01);
+                bv = _mm512_set1_pd(b1[c]);
+                c10 = _mm512_fmadd_pd(a0, bv, c10);
+                c11 = _mm512_fmadd_pd(a1, bv, c11);
+                bv = _mm512_set1_pd(b2[c]);
+                c20 = _mm512_fmadd_pd(a0, bv, c20);
+                c21 = _mm512_fmadd_pd(a1, bv, c21);
+                bv = _mm512_set1_pd(b3[c]);
+                c30 = _mm512_fmadd_pd(a0, bv, c30);
+                c31 = _mm512_fmadd_pd(a1, bv, c31);
+            }
+            double* cc = C + (size_t)j0 * ldc + i0;
+            _mm512_mask_storeu_pd(cc, k0, c00);
+            _mm512_mask_storeu_pd(cc + 8, k1, c01);
+            _mm512_mask_storeu_pd(cc + ldc, k0, c10);
+            _mm512_mask_storeu_pd(cc + ldc + 8, k1, c11);
+            _mm512_mask_storeu_pd(cc + 2 * (size_t)ldc, k0, c20);
+            _mm512_mask_storeu_pd(cc + 2 * (size_t)ldc + 8, k1, c21);
+            _mm512_mask_storeu_pd(cc + 3 * (size_t)ldc, k0, c30);
+            _mm512_mask_storeu_pd(cc + 3 * (size_t)ldc + 8, k1, c31);
+        }
+    }
+    for (; j0 < n; ++j0) {
+        const double* bj = B + (size_t)j0 * ldb;
+        double* cj = C + (size_t)j0 * ldc;
+        for (int i0 = 0; i0 < m; i0 += 8) {
+            const int r = m - i0;
+            const __mmask8 k0 = (__mmask8)(r >= 8 ? 0xFF : (1u << r) - 1u);
+            __m512d c0 = _mm512_setzero_pd();
+            for (int c = 0; c < kk; ++c)
+                c0 = _mm512_fmadd_pd(_mm512_maskz_loadu_pd(k0, A + (size_t)c * lda + i0), _mm512_set1_pd(bj[c]), c0);
+            _mm512_mask_storeu_pd(cj + i0, k0, c0);
+        }
+    }
+}
+
+static bool use_avx512() {
+    static const bool v = [] {
+        const char* e = getenv("TKHIP_HOST_AVX512");
+        return !(e && e[0] == '0') && __builtin_cpu_supports("avx512f");
+    }();
+    return v;
+}
+
 static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, const double* __restrict B, int ldb,
                     double* __restrict C, int ldc) {
+    if (use_avx512()) {
+        gemm_nn_512(m, n, kk, A, lda, B, ldb, C, ldc);
+        return;
+    }
     int j0 = 0;
     for (; j0 + 4 <= n; j0 += 4) {
         const double* b0 = B + (size_t)j0 * ldb;

@@ -530,3 +530,49 @@ def test_evaluation_split_over_helpers_is_bitwise_serial(monkeypatch, cls, sym):
                     assert np.array_equal(x, y, equal_nan=True)
     finally:
         sv.close()
+
+
+def test_host_gemm_avx512_bitwise_avx2():
+    import sys
+    """The host GEMM's AVX-512 kernel (zmm blocks, masked row edges) and its AVX2 kernel form
+    every product entry as the same k-ordered FMA chain: a nonsymmetric and a symmetric
+    iteration evaluation give the same bits with either (TKHIP_HOST_AVX512=0 / 1)."""
+    import json
+    code = r'''
+import sys, json
+sys.path[:0] = [%r, %r, %r]
+import numpy as np, tkamd
+import _fake_device as FD
+out = []
+for cls, sym in (("ConvDiff", False), ("Laplace", True)):
+    d, n, K = 4, 300, 26
+    rng = np.random.default_rng(7)
+    b = [x / np.linalg.norm(x) for x in (rng.random(n) for _ in range(d))]
+    inst = tkamd.SymInstance if sym else tkamd.NonSymInstance
+    A = tkamd.KroneckerMatrix.gallery(inst, d, n, cls)
+    td = tkamd.TensorArnoldi(A, K, backend=FD.backend)
+    td.orthonormalize_first(b)
+    f = FD.FakeDecomposition(td, b)
+    recs = [f.init()] + [f.step(j) for j in range(K)]
+    T = tkamd.compressed.IterationTables(A, K, 1e-9, d)
+    sv = tkamd.compressed.NativeSolver(td.method, d, K, sym, 1.0, T)
+    sv.apply(-1, recs[0])
+    for j in range(K):
+        sv.apply(j, recs[j + 1])
+    for k in range(2, K + 1):
+        if T.rank[k - 1] < 1:
+            continue
+        r = sv.evaluate(k)
+        lam, Y = sv.solution(k)
+        out.append([float(x).hex() for x in r] + [float(x).hex() for x in np.concatenate([np.ravel(y) for y in Y])])
+    sv.close()
+print(json.dumps(out))
+''' % (os.path.join(ROOT, "tensorkrylov.jl_amd"), ROOT, os.path.join(ROOT, "tests"))
+    res = {}
+    for v in ("0", "1"):
+        env = dict(os.environ, TKHIP_HOST_AVX512=v)
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        res[v] = json.loads(p.stdout.strip().splitlines()[-1])
+    assert len(res["0"]) > 10
+    assert res["0"] == res["1"]
