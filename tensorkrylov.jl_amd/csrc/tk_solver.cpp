@@ -189,11 +189,13 @@ static int tail_threads() {
     return v;
 }
 
-// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers
+// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers.  8: the
+// evaluations that pile up behind a short sweep get the helpers too (C4 emulated N = 8 rank 0
+// 0.79-0.83 -> 0.84-0.89 of the device rate; profiles/r04/e2e/host_avx512_tail_iters_ab.txt)
 static int tail_iters() {
     static const int v = [] {
         const char* e = getenv("TKHIP_SOLVER_TAIL_ITERS");
-        return e ? std::max(1, std::min(64, atoi(e))) : 2;
+        return e ? std::max(1, std::min(64, atoi(e))) : 8;
     }();
     return v;
 }
