@@ -469,7 +469,6 @@ __attribute__((target("avx512f"))) static void gemm_nn_512(int m, int n, int kk,
 static bool use_avx512() {
     static const bool v = [] {
         const char* e = getenv("TKHIP_HOST_AVX512");
-        __builtin_cpu_init();
         return !(e && e[0] == '0') && __builtin_cpu_supports("avx512f");
     }();
     return v;
