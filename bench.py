@@ -110,7 +110,7 @@ def main():
                          "the rank holding the tracked factor 1)")
     ap.add_argument("--no-end-to-end", action="store_true",
                     help="skip the (untimed) full-driver measurement reported as end_to_end")
-    ap.add_argument("--e2e-reps", type=int, default=3,
+    ap.add_argument("--e2e-reps", type=int, default=5,
                     help="end-to-end solves; end_to_end reports the median (one solve is a few ms)")
     ap.add_argument("--pmc-mode", action="store_true",
                     help="run exactly one untimed sweep (for rocprofv3 --pmc passes)")
