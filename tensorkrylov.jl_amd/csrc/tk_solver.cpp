@@ -189,13 +189,22 @@ static int tail_threads() {
     return v;
 }
 
-// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers (they
-// spin from the dispatch of the first of them).  2; 8 lets the evaluations that pile up behind
+// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers.  2; 8 lets the evaluations that pile up behind
 // a short sweep use them too (C4 emulated N = 8: 0.79-0.84 -> 0.84-0.89 of the device rate)
 // but cost the N = 1 lines 1-2 % (C4 0.960 -> 0.948; profiles/r04/e2e/host_avx512_tail_iters_ab.txt)
 static int tail_iters() {
     static const int v = [] {
         const char* e = getenv("TKHIP_SOLVER_TAIL_ITERS");
+        return e ? std::max(1, std::min(64, atoi(e))) : 2;
+    }();
+    return v;
+}
+
+// TKHIP_SOLVER_HOT_ITERS: from the dispatch of iteration klast - this on, the helpers spin
+// instead of blocking (earlier splits wake them through their condition variable)
+static int hot_iters() {
+    static const int v = [] {
+        const char* e = getenv("TKHIP_SOLVER_HOT_ITERS");
         return e ? std::max(1, std::min(64, atoi(e))) : 2;
     }();
     return v;
@@ -591,7 +600,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             std::lock_guard<std::mutex> lk(pool.mu);
             pool.done[w] = 0;
         }
-        if (hp && k >= klast - tail_iters()) hp->set_hot(true);
+        if (hp && k >= klast - hot_iters()) hp->set_hot(true);
         {
             std::lock_guard<std::mutex> lk(workers[w]->mu);
             workers[w]->ws.nthreads = k > klast - tail_iters() ? tail : 1;
