@@ -189,9 +189,10 @@ static int tail_threads() {
     return v;
 }
 
-// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers.  2; 8 lets the evaluations that pile up behind
-// a short sweep use them too (C4 emulated N = 8: 0.79-0.84 -> 0.84-0.89 of the device rate)
-// but cost the N = 1 lines 1-2 % (C4 0.960 -> 0.948; profiles/r04/e2e/host_avx512_tail_iters_ab.txt)
+// TKHIP_SOLVER_TAIL_ITERS: how many of the last iterations may split over the helpers.  2; 8
+// (with the helpers spinning for all 8) lets the evaluations that pile up behind a short sweep
+// use them too (C4 emulated N = 8: 0.79-0.84 -> 0.84-0.89 of the device rate) but cost the
+// N = 1 lines 1-2 % (C4 0.960 -> 0.948; profiles/r04/e2e/host_avx512_tail_iters_ab.txt)
 static int tail_iters() {
     static const int v = [] {
         const char* e = getenv("TKHIP_SOLVER_TAIL_ITERS");
