@@ -3,6 +3,7 @@
 // launch set over all of this rank's factors), the one RCCL all-reduce per step, and
 // HIP-event timing.  No host pointer is retained after a call returns.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <rccl/rccl.h>
 
 #include <math.h>
@@ -22,6 +23,17 @@
 #include "../../include/tk.h"
 #include "tk_internal.h"
 #include "tk_xsched.h"
+
+// host polls of device-written words in host-mapped memory: TK_POLL_PAUSE=1 issues a pause
+// between reads (fewer reads of lines the GPU is writing over the fabric)
+#ifndef TK_POLL_PAUSE
+#define TK_POLL_PAUSE 1
+#endif
+#if TK_POLL_PAUSE
+#define TK_POLL_RELAX() _mm_pause()
+#else
+#define TK_POLL_RELAX() do { } while (0)
+#endif
 
 using namespace tk;
 
@@ -1801,6 +1813,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
             for (int f = 0; f < dc->nf; ++f) {
                 long spins = 0;
                 while (__atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want) {
+                    TK_POLL_RELAX();
                     if (++spins % 4096 == 0) {
                         // the device may have failed: surface its error instead of spinning (both
                         // factor-group streams: the records are late only if neither runs)
@@ -1829,6 +1842,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
             const unsigned long long want = dc->xslot_seq[sl];
             long spins = 0;
             while (__atomic_load_n(dc->xdone + sl, __ATOMIC_ACQUIRE) < want) {
+                TK_POLL_RELAX();
                 if (++spins % 4096 == 0) {
                     hipError_t e = hipStreamQuery(c->xstream);
                     if (e != hipSuccess && e != hipErrorNotReady)
@@ -1915,6 +1929,7 @@ static tk_status gram_wait(tk_decomp* dc, hipStream_t s, unsigned long long want
     long spins = 0;
     Deadline dl;
     while (__atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want) {
+        TK_POLL_RELAX();
         if (++spins % 4096 == 0) {
             hipError_t e = hipStreamQuery(s);
             if (e != hipSuccess && e != hipErrorNotReady) return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
