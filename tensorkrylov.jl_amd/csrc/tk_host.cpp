@@ -200,9 +200,7 @@ static void gemm_nn(int m, int n, int kk, const double* __restrict A, int lda, c
 // iteration's host time at C4)
 static void matmul(int n, const double* A, const double* B, double* C) { gemm_nn(n, n, n, A, n, B, n, C, n); }
 
-static bool use_avx512();
-template <int V>   // (V: instantiation tag only; the body is inlined into the two entry points)
-static inline __attribute__((always_inline)) bool lu_solve_body(int n, Vec& A, Vec& B) {
+static bool lu_solve(int n, Vec& A, Vec& B) {
     // solve A X = B (n x n each), partial pivoting; B overwritten by X.  Columns are separate
     // arrays to the compiler (restrict): every inner loop is an axpy it vectorizes.
     std::vector<int> piv(n);
@@ -259,10 +257,6 @@ static inline __attribute__((always_inline)) bool lu_solve_body(int n, Vec& A, V
         for (int i = 0; i < n; ++i) B[(size_t)j * n + i] = X[(size_t)i * n + j];
     return true;
 }
-// the same loops vectorized for zmm where the CPU has AVX-512 (each element's arithmetic is
-// unchanged, so the same bits as the AVX2 build of the body)
-__attribute__((target("avx512f"))) static bool lu_solve_512(int n, Vec& A, Vec& B) { return lu_solve_body<1>(n, A, B); }
-static bool lu_solve(int n, Vec& A, Vec& B) { return use_avx512() ? lu_solve_512(n, A, B) : lu_solve_body<0>(n, A, B); }
 
 // exp(c A) by Pade approximants of degree 3/5/7/9/13 with scaling and squaring (Higham 2005,
 // the method of Julia's LinearAlgebra.exp!).  The even powers A^2, A^4, A^6, A^8 of the
