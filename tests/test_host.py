@@ -576,3 +576,34 @@ print(json.dumps(out))
         res[v] = json.loads(p.stdout.strip().splitlines()[-1])
     assert len(res["0"]) > 10
     assert res["0"] == res["1"]
+
+
+def test_orthogonality_losses_native_edges_and_lower_triangle():
+    """tk_orthogonality_losses (the sum the native loop applies to the Gram it reads) reads the
+    lower triangle only, in the order tk_solver_evaluate sums a tracked factor's Gram rows:
+    a garbage upper triangle changes nothing; K = 1 and an exact identity give exact values;
+    K = 0 is accepted."""
+    import ctypes
+    from tkamd import _lib as L
+    from tkamd.compressed import orthogonality_losses_from_gram
+    rng = np.random.default_rng(3)
+    K = 23
+    V = np.linalg.qr(rng.standard_normal((200, K)))[0] + 1e-9 * rng.standard_normal((200, K))
+    G = V.T @ V
+    Gu = np.tril(G) + np.triu(rng.standard_normal((K, K)), 1)     # upper triangle: noise
+    assert np.array_equal(orthogonality_losses_from_gram(G), orthogonality_losses_from_gram(Gu))
+    # the sequential sum, restated (the library contracts products into FMAs: rounding-level
+    # differences only)
+    acc, ref = 0.0, []
+    for c in range(K):
+        dd = G[c, c] - 1.0
+        off = 0.0
+        for i in range(c):
+            off += G[c, i] * G[c, i]
+        acc += dd * dd + 2.0 * off
+        ref.append(math.sqrt(acc))
+    assert np.allclose(orthogonality_losses_from_gram(G), np.array(ref), rtol=1e-13, atol=0)
+    assert np.array_equal(orthogonality_losses_from_gram(np.eye(7)), np.zeros(7))
+    assert orthogonality_losses_from_gram(np.array([[1.5]]))[0] == 0.5
+    out = np.zeros(1)
+    assert L.lib().tk_orthogonality_losses(0, L.dptr(out), L.dptr(out)) == 0
