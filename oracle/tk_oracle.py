@@ -485,17 +485,22 @@ class ConvergenceData:
 
 
 def tensorkrylov(A_cscs, b, tol, nmax, method, cls, symmetric, tables=None,
-                 A_dense=None, step_hook=None):
+                 A_dense=None, step_hook=None, factor=None, threads=1):
     """tensorkrylov!  (src/tensor_krylov_method.jl:36-125).
     method in {"TensorArnoldi", "TensorLanczos", "TensorLanczosReorth"}.
+    factor: the per-factor state class (default Factor, NumPy); tk_ref.CFactor steps the
+    factors in the C restatement instead (full-size tests: same MGS2 order, compiled).
+    threads > 1 steps the factors concurrently (independent per factor, so the same
+    results; useful only with CFactor, whose C calls release the GIL).
     Returns (ConvergenceData, x or None, factors)."""
     d = len(A_cscs)
     n = len(b[0])
     conv = ConvergenceData(nmax)
     b_norm = math.sqrt(np.prod([np.dot(bs, bs) for bs in b]))    # kronprodnorm
-    fs = [Factor(A_cscs[s], b[s], nmax) for s in range(d)]
-    step = {"TensorArnoldi": Factor.arnoldi_mgs, "TensorLanczos": Factor.lanczos_ttr,
-            "TensorLanczosReorth": Factor.lanczos_reorth}[method]
+    factor = factor or Factor
+    fs = [factor(A_cscs[s], b[s], nmax) for s in range(d)]
+    step = {"TensorArnoldi": factor.arnoldi_mgs, "TensorLanczos": factor.lanczos_ttr,
+            "TensorLanczosReorth": factor.lanczos_reorth}[method]
     for f in fs:                                                  # orthonormalize!(td, b) :53
         step(f, 1)
     btilde = [np.zeros(n) for _ in range(d)]
@@ -505,9 +510,16 @@ def tensorkrylov(A_cscs, b, tol, nmax, method, cls, symmetric, tables=None,
         tables = ExpSumTables()
     r_norm = math.inf
     x = None
+    pool = None
+    if threads > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        pool = ThreadPoolExecutor(threads)
     for k in range(2, nmax + 1):                                  # :63
-        for f in fs:
-            step(f, k)                                            # :66
+        if pool is not None:
+            list(pool.map(lambda f: step(f, k), fs))              # :66
+        else:
+            for f in fs:
+                step(f, k)                                        # :66
         for s in range(d):                                        # update_rhs! :71
             btilde[s][k - 1] = np.dot(fs[s].V[:, k - 1], b[s])
         minor = None if A_dense is None else A_dense[:k, :k]

@@ -85,6 +85,27 @@ class RefFactor:
         return a.value, bt.value
 
 
+class CFactor:
+    """tk_oracle.Factor's interface (1-based k, V, H) over RefFactor, so that
+    tk_oracle.tensorkrylov(..., factor=CFactor) steps its factors in the C restatement:
+    the MGS2 step of src/orthogonal_bases.jl:15-37 and the TTR step of :39-67 in the
+    reference's operation order, compiled (the full-size n = 2^20 driver tests)."""
+
+    def __init__(self, csc, b, kmax):
+        self._f = RefFactor(csc, b, kmax)
+        self.V = self._f.V                 # n x (kmax+1), column-major
+        self.H = self._f.H                 # (kmax+2) x (kmax+1)
+
+    def arnoldi_mgs(self, k):
+        self._f.arnoldi_step(k - 1)
+
+    def lanczos_ttr(self, k):
+        self._f.lanczos_step(k - 1)
+
+    def lanczos_reorth(self, k, force=None):
+        raise NotImplementedError("LanczosReorth: use tk_oracle.Factor")
+
+
 def baseline(csc, n, d, K, seconds=15.0):
     """CPU baseline for bench.py: the C restatement's full K-step Arnoldi (MGS2) sweep,
     1 thread, on the benchmark's factors (b_s ~ U(0,1), seed 1000+s, as on the GPU) one

@@ -182,10 +182,29 @@ static tk_status wait_expired(tk_ctx* c, const char* what, int slot) {
                 what, wait_limit_s(), slot, slot - 1, c->rank, c->nranks, comm_state(c));
 }
 
+// Without a communicator (one GPU) waits are plain synchronisations: queued work of any
+// length is waited for and the context is never marked stuck.  TKHIP_LOCAL_WAIT_S > 0 bounds
+// them too (a device hang then returns TK_ERR_HIP naming the wait instead of blocking the
+// host; the context stays usable) -- off by default: a long legitimate queue must not fail
+static double local_limit_s() {
+    static const double v = [] {
+        const char* e = getenv("TKHIP_LOCAL_WAIT_S");
+        const double x = e ? atof(e) : 0.0;
+        return x > 0 ? x : 0.0;
+    }();
+    return v;
+}
+// the limit a wait of this context has: TKHIP_WAIT_S with peers, else TKHIP_LOCAL_WAIT_S (0: none)
+static double ctx_wait_limit(const tk_ctx* c) { return c->comm ? wait_limit_s() : local_limit_s(); }
+
 struct Deadline {
     typedef std::chrono::steady_clock clk;
     clk::time_point t0 = clk::now();
     double lim = wait_limit_s();
+    Deadline() = default;
+    explicit Deadline(double l) : lim(l) {}
+    // (lim 0: never expires)
+    bool over() const { return lim > 0 && elapsed() > lim; }
     double elapsed() const { return std::chrono::duration<double>(clk::now() - t0).count(); }
     // true once expired; backs off to short sleeps after the first millisecond
     bool tick() {
@@ -199,32 +218,36 @@ struct Deadline {
 // hipStreamSynchronize with a deadline -- only where another rank can be involved: without a
 // communicator (one GPU) queued work of any length is waited for plainly, and never marks the
 // context stuck
+static tk_status local_expired(const char* what, double lim) {
+    return fail(TK_ERR_HIP, "%s: device work not complete after %.0f s (TKHIP_LOCAL_WAIT_S)", what, lim);
+}
+
 static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int slot = -1) {
-    if (!c->comm) {
+    if (!c->comm && local_limit_s() <= 0) {
         const hipError_t e = hipStreamSynchronize(s);
         return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
     }
-    Deadline dl;
+    Deadline dl(ctx_wait_limit(c));
     for (;;) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return TK_OK;
         if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-        if (dl.tick()) return wait_expired(c, what, slot);
+        if (dl.tick()) return c->comm ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
     }
 }
 
 // hipEventSynchronize with a deadline
 static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int slot = -1) {
-    if (!c->comm) {
+    if (!c->comm && local_limit_s() <= 0) {
         const hipError_t e = hipEventSynchronize(ev);
         return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
     }
-    Deadline dl;
+    Deadline dl(ctx_wait_limit(c));
     for (;;) {
         const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return TK_OK;
         if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-        if (dl.tick()) return wait_expired(c, what, slot);
+        if (dl.tick()) return c->comm ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
     }
 }
 
@@ -1806,7 +1829,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     if (hosted) {
         // wait for the steps that wrote these slots only (later steps may be queued or
         // running), then read their records from host-mapped memory
-        Deadline dl;
+        Deadline dl(ctx_wait_limit(c));
         for (int sl = s0; sl < s1; ++sl) {
             const unsigned long long want = dc->slot_seq[sl];
             const unsigned long long* w = dc->hdone + (size_t)sl * dc->nf;
@@ -1823,8 +1846,8 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
                             return fail(TK_ERR_HIP, "waiting for step records: %s", hipGetErrorString(e));
                         if (e == hipSuccess && __atomic_load_n(w + f, __ATOMIC_ACQUIRE) < want)
                             return fail(TK_ERR_STATE, "step records of slot %d never arrived", sl);
-                        // (a deadline only where a peer could hold the queue back)
-                        if (c->comm && dl.elapsed() > dl.lim)
+                        // (a deadline where a peer could hold the queue back, or TKHIP_LOCAL_WAIT_S)
+                        if (dl.over())
                             return fail(TK_ERR_HIP, "step records of slot %d: not complete after %.0f s", sl, dl.lim);
                     }
                 }
@@ -1927,7 +1950,7 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
 static tk_status gram_wait(tk_decomp* dc, hipStream_t s, unsigned long long want) {
     tk_ctx* c = dc->ctx;
     long spins = 0;
-    Deadline dl;
+    Deadline dl(ctx_wait_limit(c));
     while (__atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want) {
         TK_POLL_RELAX();
         if (++spins % 4096 == 0) {
@@ -1935,7 +1958,7 @@ static tk_status gram_wait(tk_decomp* dc, hipStream_t s, unsigned long long want
             if (e != hipSuccess && e != hipErrorNotReady) return fail(TK_ERR_HIP, "tk_decomp_gram: %s", hipGetErrorString(e));
             if (e == hipSuccess && __atomic_load_n(dc->gram_done, __ATOMIC_ACQUIRE) < want)
                 return fail(TK_ERR_STATE, "tk_decomp_gram: the result never arrived");
-            if (c->comm && dl.elapsed() > dl.lim)
+            if (dl.over())
                 return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
         }
     }
@@ -2042,6 +2065,11 @@ tk_status tk_decomp_gram_ahead(tk_decomp* dc, int* k_out) { TK_API_BEGIN
     k = std::min(std::min(k, 64), dc->kmax + 1);
     if (k < 2) return TK_OK;
     HIPCHK(hipSetDevice(c->device));
+    // the last step's deferred bookkeeping (its record, host mirror and exchange signal) goes
+    // first: behind the SYRK, the final iteration's record -- and with peers that slot's
+    // all-reduce -- would wait for the whole Gram.  Local: no collective
+    tk_status st = bk_flush(dc);
+    if (st) return st;
     GJOIN(dc);
     if (!dc->gram_scr) HIPCHK(hipMalloc((void**)&dc->gram_scr, gram_scratch_doubles(dc->ntiles) * sizeof(double)));
     hipStream_t s = c->stream;

@@ -596,11 +596,14 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             if (h) h->set_hot(false);
         }
     } hot_off{hp};
+    // per worker: the iteration submitted and not yet consumed (quiesce waits for its result)
+    std::vector<int> inflight(workers.size(), 0);
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
             pool.done[w] = 0;
         }
+        inflight[w] = k;
         if (hp && k >= klast - hot_iters()) hp->set_hot(true);
         {
             std::lock_guard<std::mutex> lk(workers[w]->mu);
@@ -613,17 +616,19 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     auto wait_done = [&](int w, int k) {
         std::unique_lock<std::mutex> lk(pool.mu);
         pool.cv.wait(lk, [&] { return pool.done[w] == k; });
+        inflight[w] = 0;
     };
     // the end of a run: jobs still in flight finish (their results are discarded); the
-    // threads stay for the next run or tk_solver_destroy
+    // threads stay for the next run or tk_solver_destroy.  A worker clears its job before it
+    // publishes pool.done (the other order could erase a job submitted in between), so the
+    // wait is for the published result itself: a late pool.done write of this run's last
+    // iterations must not land after the next run has reset pool.done
     auto quiesce = [&] {
-        for (auto& wk : workers) {
-            std::unique_lock<std::mutex> lk(wk->mu);
-            while (wk->job > 0) {
-                lk.unlock();
-                std::this_thread::yield();
-                lk.lock();
-            }
+        std::unique_lock<std::mutex> lk(pool.mu);
+        for (size_t w = 0; w < inflight.size(); ++w) {
+            if (!inflight[w]) continue;
+            pool.cv.wait(lk, [&] { return pool.done[w] == inflight[w]; });
+            inflight[w] = 0;
         }
     };
     int k_dispatch = kfirst;

@@ -167,3 +167,23 @@ def test_all_cores_baseline_sweep_matches_port():
         scale = np.abs(f.H).max()
         assert np.abs(H[:K + 1, :K] - f.H[:K + 1, :K]).max() <= 1e-12 * scale
         assert np.abs(V - f.V).max() <= 1e-12
+
+
+def test_oracle_driver_with_c_factors_matches_numpy_factors():
+    """tk_oracle.tensorkrylov(..., factor=tk_ref.CFactor) -- the form the full-size C2
+    north-star test uses -- gives the NumPy-factor driver's trajectory (the two factor
+    restatements agree to rounding, src/orthogonal_bases.jl:15-37)."""
+    from oracle import tk_ref
+    d, n, K = 4, 200, 30
+    csc = O.gallery_csc(n, "Laplace")
+    rng = np.random.default_rng(11)
+    b = O.normalize_rhs([rng.random(n) for _ in range(d)])
+    c_np, _, _ = O.tensorkrylov([csc] * d, b, 1e-9, K, "TensorArnoldi", "Laplace", True)
+    c_c, _, fs = O.tensorkrylov([csc] * d, b, 1e-9, K, "TensorArnoldi", "Laplace", True,
+                                factor=tk_ref.CFactor)
+    assert isinstance(fs[0], tk_ref.CFactor)
+    assert c_np.niterations == c_c.niterations
+    r_np = np.array(c_np.relative_residual_norm[1:])
+    r_c = np.array(c_c.relative_residual_norm[1:])
+    assert np.abs(r_c - r_np).max() <= 1e-11 * r_np.max()
+    assert np.abs(np.array(c_c.orthogonality_data[1:]) - np.array(c_np.orthogonality_data[1:])).max() <= 1e-13
