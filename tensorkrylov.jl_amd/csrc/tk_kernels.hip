@@ -76,13 +76,16 @@ __device__ __forceinline__ rsrc_t mkrsrc(const void* p, uint32_t bytes) {
 }
 // V is streamed once per pass and never re-read from cache within a step: non-temporal
 // loads (aux = 2, `nt`) measured 3-5 % faster than the default policy (tools/bwprobe.hip).
+#ifndef TK_V_AUX
+#define TK_V_AUX 2
+#endif
 __device__ __forceinline__ double bld(rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 2));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, TK_V_AUX));
 }
 
 typedef double d2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ d2_t bld2(rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(d2_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 2));
+    return __builtin_bit_cast(d2_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, TK_V_AUX));
 }
 // Paired-column tile layout: element offset of (row t, column c) inside a tile, byte
 // offset of column c relative to thread t's pair base (t*16), tile stride, and the
