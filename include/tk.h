@@ -340,6 +340,32 @@ tk_status tk_solver_prepare(tk_solver* sv, int nthreads);
  * *k_end may still run; their results are not read. */
 tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, int depth, int nthreads,
                         double* relres, double* projres, double* orth, int* k_end, int* outcome);
+/* Evaluation split over the ranks of one node (the reference evaluates every
+ * iteration itself, src/tensor_krylov_method.jl:72-103): after tk_solver_share, iteration k's
+ * compressed solve + residual is evaluated by rank (k mod nranks) only, and every other rank
+ * reads its (r_comp, r_norm, relres, orthogonality, status) from a node-local mailbox -- POSIX
+ * shared memory /dev/shm/tkhip_ev_<key>, created by rank 0, unlinked as soon as every rank has
+ * attached (so nothing is left behind).  Every rank holds the same host mirror (the records
+ * all-reduce), so the result is bitwise what it would have computed, and convergence /
+ * breakdown are decided at the same iteration on every rank.  Collective: every rank calls it
+ * with the same key (e.g. derived from the RCCL unique id) and nranks; waits are bounded by
+ * TKHIP_WAIT_S.  tk_solver_run splits only when every rank of the decomposition's exchange
+ * shares (agreed at the run's start); on convergence at an iteration another rank evaluated,
+ * the run evaluates it locally for tk_solver_solution.  nranks = 1 turns the split off. */
+tk_status tk_solver_share(tk_solver* sv, const char* key, int nranks, int rank);
+/* Diagnostic (bench.py --emulate-ranks): the split on one rank, with the results of the
+ * iterations other ranks would own taken from `results` ([kmax][6], tk_solver_results of a
+ * full run), each released no earlier than its record's arrival plus the evaluation time that
+ * run measured for it.  nranks = 1 turns it off. */
+tk_status tk_solver_share_emulated(tk_solver* sv, int nranks, int rank, const double* results);
+/* Per iteration k (row k-1) of the last tk_solver_run: r_comp, r_norm, relres, orthogonality
+ * loss, status (TK_OK / TK_BREAKDOWN), this rank's evaluation time in us (-1 if another rank
+ * evaluated it); NaN rows for iterations the run did not consume.  out: [kmax][6]. */
+tk_status tk_solver_results(tk_solver* sv, double* out);
+/* tk_solver_evaluate under the split (a host-driven loop, one call per k in order on every
+ * rank): the owner evaluates and posts, the others wait for its result; out4 and the status as
+ * tk_solver_evaluate.  Without tk_solver_share it is tk_solver_evaluate. */
+tk_status tk_solver_evaluate_shared(tk_solver* sv, int k, double* out4);
 /* orthogonality_loss(V, k) = norm(V[:, 1:k]' V[:, 1:k] - I) for k = 1..K from ONE Gram matrix
  * G = V[:, 1:K]' V[:, 1:K] (K x K column-major, lower triangle read) into out[K]
  * (src/orthogonal_bases.jl:250-257, called per iteration at src/tensor_krylov_method.jl:103):

@@ -1329,7 +1329,18 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
         HIPCHK(hipStreamWaitValue64(c->xstream, dc->stallw, dc->stall_v + 1, hipStreamWaitValueGte,
                                     0xFFFFFFFFFFFFFFFFull));
     {
+        // TKHIP_TEST_XCH_DELAY_US (test / prediction only): hold each all-reduce back this long
+        // on the exchange stream -- what an 8-peer xGMI all-reduce costs beyond a 1-rank one --
+        // so that bench.py --emulate-ranks prices collective latency
+        static const double delay_us = [] {
+            const char* e = getenv("TKHIP_TEST_XCH_DELAY_US");
+            return e ? std::max(0.0, atof(e)) : 0.0;
+        }();
         Timer tm(c, TCLS_XCH, 2, c->xstream);
+        if (delay_us > 0) {
+            launch_delay_us(delay_us, c->xstream);
+            LAUNCHCHK("xch delay");
+        }
         NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
     }
     HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));

@@ -133,6 +133,7 @@ constexpr int ARN_D1_JMAX = 63;
 // launchers (tk_kernels.hip)
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
                            unsigned long long seq, hipStream_t s);
+void launch_delay_us(double us, hipStream_t s);   // test-only (TKHIP_TEST_XCH_DELAY_US)
 void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, int mode,
                    hipStream_t s);
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);

@@ -3061,6 +3061,17 @@ __global__ __launch_bounds__(TPB) void k_mirror_records(const double* __restrict
     if (threadIdx.x == 0)
         for (int q = 0; q < nslots; ++q) __hip_atomic_store(done + q, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Test-only latency stand-in (TKHIP_TEST_XCH_DELAY_US, tk_abi.cpp exchange_range): one wave
+// that waits `ticks` of the 100 MHz wall clock on the exchange stream ahead of an all-reduce,
+// so a 1-rank communicator's exchange takes as long as an 8-peer one would.
+// Nothing is read or written.
+__global__ __launch_bounds__(64) void k_delay(uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+void launch_delay_us(double us, hipStream_t s) {
+    hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (uint64_t)(us * 100.0 + 0.5));
+}
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
                            unsigned long long seq, hipStream_t s) {
     hipLaunchKernelGGL(k_mirror_records, dim3(1), dim3(TPB), 0, s, src, dst, cnt, done, nslots, seq);

@@ -12,8 +12,12 @@
 // iterate is bitwise the one a sequential loop computes (the worker count changes only
 // throughput).  The spectral bounds and exp-sum ranks/coefficients depend on A and tol
 // only; the caller passes them per k (tk_solver_create).
+#include <fcntl.h>
 #include <math.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -211,6 +215,43 @@ static int hot_iters() {
     return v;
 }
 
+// ------------------------------------------------------------------ evaluation split
+// With several ranks every rank holds the same host mirror (the records all-reduce gives each
+// every factor's record), so iteration k's evaluation is the same pure function on every
+// rank: rank (k mod nranks) evaluates it and the others read its result.  The
+// results travel through a node-local mailbox -- one POSIX shared-memory file per job, one
+// 64-byte entry per iteration, a generation word written last -- not through the records
+// all-reduce: a result posted in a later step's slot would reach the other ranks only with
+// that step's records, i.e. every convergence / breakdown decision L steps late, and the last
+// L iterations would need an extra collective.  The mailbox costs a cache line per iteration.
+struct MailHeader {
+    uint64_t magic, nranks, kmax, attached;
+    uint64_t pad[4];
+};
+struct MailEntry {                 // one per iteration k (index k)
+    uint64_t gen;                  // written last (release): the run this entry belongs to
+    double rc, rn, rel, orth;
+    int64_t status;
+    uint64_t pad[2];
+};
+static_assert(sizeof(MailHeader) == 64 && sizeof(MailEntry) == 64, "one cache line each");
+static const uint64_t MAIL_MAGIC = 0x746b6869705f6576ull;   // "tkhip_ev"
+
+struct Share {
+    int nranks = 1, rank = 0;
+    MailHeader* hdr = nullptr;     // mailbox (real ranks)
+    MailEntry* ent = nullptr;
+    size_t bytes = 0;
+    std::vector<double> table;     // emulation: a full run's results [k-1][6] (tk_solver_results)
+    uint64_t gen = 0;              // this run's generation (every rank counts runs alike)
+    int last_k = 1 << 30;          // (tk_solver_evaluate_shared: a new generation when k restarts)
+    bool on() const { return nranks > 1; }
+    bool owner(int k) const { return nranks <= 1 || k % nranks == rank; }
+};
+
+// per-iteration results of the last run, [k-1][6] = r_comp, r_norm, rel, orth, status, eval us
+enum { RES_RC, RES_RN, RES_REL, RES_ORTH, RES_ST, RES_US, RES_N };
+
 }  // namespace
 
 struct tk_solver {
@@ -235,7 +276,79 @@ struct tk_solver {
     Pool pool;
     std::vector<std::unique_ptr<Worker>> workers;
     std::unique_ptr<Helpers> helpers;   // (tail_threads() > 1)
+    Share share;
+    std::vector<double> results;        // [kmax][RES_N] of the last run (NaN: not consumed)
 };
+
+static void mail_post(tk_solver* sv, const IterResult& r) {
+    MailEntry* e = sv->share.ent;
+    if (!e || r.k < 0 || r.k > sv->kmax) return;
+    e += r.k;
+    e->rc = r.r_comp;
+    e->rn = r.r_norm;
+    e->rel = r.rel;
+    e->orth = r.orth;
+    e->status = r.status;
+    __atomic_store_n(&e->gen, sv->share.gen, __ATOMIC_RELEASE);
+}
+
+static double wait_limit_solver_s() {
+    const char* e = getenv("TKHIP_WAIT_S");
+    const double v = e ? atof(e) : 120.0;
+    return v > 0 ? v : 120.0;
+}
+
+// iteration k's result from its owner: the mailbox (bounded by TKHIP_WAIT_S), or in
+// emulation the full run's table, released no earlier than the owner would have had it (the
+// record's arrival here + the owner's evaluation time in that run)
+static tk_status mail_take(tk_solver* sv, int k, IterResult& out, std::chrono::steady_clock::time_point t_rec) {
+    Share& sh = sv->share;
+    out.k = k;
+    out.lam.clear();
+    out.Y.clear();
+    if (sh.ent) {
+        const MailEntry* e = sh.ent + k;
+        const auto t0 = std::chrono::steady_clock::now();
+        const double lim = wait_limit_solver_s();
+        for (long spins = 0; __atomic_load_n(&e->gen, __ATOMIC_ACQUIRE) != sh.gen; ++spins) {
+            _mm_pause();
+            if ((spins & 1023) == 1023) {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim) {
+                    char b[160];
+                    snprintf(b, sizeof b, "evaluation split: rank %d never published iteration %d (%.0f s, TKHIP_WAIT_S)",
+                             k % sh.nranks, k, lim);
+                    return tk_fail_internal(TK_ERR_RCCL, b);
+                }
+                std::this_thread::yield();
+            }
+        }
+        out.r_comp = e->rc;
+        out.r_norm = e->rn;
+        out.rel = e->rel;
+        out.orth = e->orth;
+        out.status = (int)e->status;
+        return TK_OK;
+    }
+    const double* r = &sh.table[(size_t)(k - 1) * RES_N];
+    const auto ready = t_rec + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                   std::chrono::duration<double, std::micro>(std::max(0.0, r[RES_US])));
+    while (std::chrono::steady_clock::now() < ready) _mm_pause();
+    out.r_comp = r[RES_RC];
+    out.r_norm = r[RES_RN];
+    out.rel = r[RES_REL];
+    out.orth = r[RES_ORTH];
+    out.status = (int)r[RES_ST];
+    return TK_OK;
+}
+
+static void share_close(Share& sh) {
+    if (sh.hdr) munmap(sh.hdr, sh.bytes);
+    sh.hdr = nullptr;
+    sh.ent = nullptr;
+    sh.table.clear();
+    sh.nranks = 1;
+    sh.rank = 0;
+}
 
 static void apply_record(tk_solver* sv, int j, const double* rec) {
     const int kmax = sv->kmax, m = sv->m, KP = sv->KP, KC = sv->KC;
@@ -344,6 +457,7 @@ static void worker_loop(tk_solver* sv, int w, Worker* wkp) {
         evaluate(sv, k, wk.res, wk.ws);
         wk.res.t0 = tb;
         wk.res.t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        if (sv->share.ent) mail_post(sv, wk.res);   // (split: the other ranks read it at once)
         {
             std::lock_guard<std::mutex> lk(wk.mu);
             wk.job = 0;
@@ -443,6 +557,7 @@ tk_status tk_solver_create(int method, int d, int kmax, int symmetric, double b_
     sv->gram0.assign((size_t)sv->KC * sv->KC, 0.0);
     sv->loss.assign((size_t)d * sv->KC, 0.0);
     sv->reorth.assign((size_t)d * sv->KC, 0);
+    sv->results.assign((size_t)kmax * RES_N, NAN);
     *out = sv;
     return TK_OK;
     TK_API_END
@@ -464,6 +579,7 @@ tk_status tk_solver_overlay(tk_solver* sv, int first, int nf, const double* reco
 tk_status tk_solver_destroy(tk_solver* sv) {
     if (!sv) return TK_OK;
     stop_workers(sv);
+    share_close(sv->share);
     delete sv;
     return TK_OK;
 }
@@ -519,6 +635,138 @@ tk_status tk_solver_state(tk_solver* sv, double* H_out, double* bt_out, double* 
     TK_API_END
 }
 
+tk_status tk_solver_share(tk_solver* sv, const char* key, int nranks, int rank) { TK_API_BEGIN
+    if (!sv || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !key))
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_share: bad argument");
+    share_close(sv->share);
+    if (nranks == 1) return TK_OK;
+    for (const char* p = key; *p; ++p)
+        if (!((*p >= '0' && *p <= '9') || (*p >= 'a' && *p <= 'z') || (*p >= 'A' && *p <= 'Z') || *p == '_') ||
+            p - key > 96)
+            return tk_fail_internal(TK_ERR_ARG, "tk_solver_share: key must be [0-9A-Za-z_]{1,96}");
+    char name[160];
+    snprintf(name, sizeof name, "/dev/shm/tkhip_ev_%s", key);
+    const size_t bytes = sizeof(MailHeader) + (size_t)(sv->kmax + 2) * sizeof(MailEntry);
+    const double lim = wait_limit_solver_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto expired = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > lim; };
+    char msg[256];
+    int fd = -1;
+    if (rank == 0) {
+        // create under a temporary name, initialise, then publish by rename (no rank maps a
+        // half-built file); unlinked once every rank has attached
+        char tmp[192];
+        snprintf(tmp, sizeof tmp, "%s.%d.tmp", name, (int)getpid());
+        fd = open(tmp, O_RDWR | O_CREAT | O_EXCL, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
+            if (fd >= 0) close(fd), unlink(tmp);
+            snprintf(msg, sizeof msg, "tk_solver_share: cannot create %s", tmp);
+            return tk_fail_internal(TK_ERR_STATE, msg);
+        }
+        void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m == MAP_FAILED) {
+            unlink(tmp);
+            return tk_fail_internal(TK_ERR_STATE, "tk_solver_share: mmap failed");
+        }
+        memset(m, 0, bytes);
+        MailHeader* h = (MailHeader*)m;
+        h->magic = MAIL_MAGIC;
+        h->nranks = (uint64_t)nranks;
+        h->kmax = (uint64_t)sv->kmax;
+        __atomic_store_n(&h->attached, 1, __ATOMIC_RELEASE);
+        if (rename(tmp, name) != 0) {
+            munmap(m, bytes);
+            unlink(tmp);
+            snprintf(msg, sizeof msg, "tk_solver_share: cannot publish %s", name);
+            return tk_fail_internal(TK_ERR_STATE, msg);
+        }
+        while (__atomic_load_n(&h->attached, __ATOMIC_ACQUIRE) < (uint64_t)nranks) {
+            if (expired()) {
+                unlink(name);
+                munmap(m, bytes);
+                snprintf(msg, sizeof msg, "tk_solver_share: %d of %d ranks attached to %s within %.0f s (TKHIP_WAIT_S)",
+                         (int)__atomic_load_n(&h->attached, __ATOMIC_ACQUIRE), nranks, name, lim);
+                return tk_fail_internal(TK_ERR_RCCL, msg);
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        unlink(name);   // every rank holds its mapping: nothing is left in /dev/shm
+        sv->share.hdr = h;
+    } else {
+        while ((fd = open(name, O_RDWR)) < 0) {
+            if (expired()) {
+                snprintf(msg, sizeof msg, "tk_solver_share: rank 0 never published %s within %.0f s (TKHIP_WAIT_S)", name, lim);
+                return tk_fail_internal(TK_ERR_RCCL, msg);
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        struct stat st;
+        void* m = (fstat(fd, &st) == 0 && (size_t)st.st_size == bytes)
+                      ? mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+        close(fd);
+        MailHeader* h = (MailHeader*)m;
+        if (m == MAP_FAILED || h->magic != MAIL_MAGIC || h->nranks != (uint64_t)nranks || h->kmax != (uint64_t)sv->kmax) {
+            if (m != MAP_FAILED) munmap(m, bytes);
+            snprintf(msg, sizeof msg, "tk_solver_share: %s does not describe this job (%d ranks, kmax %d)", name, nranks,
+                     sv->kmax);
+            return tk_fail_internal(TK_ERR_STATE, msg);
+        }
+        __atomic_fetch_add(&h->attached, 1, __ATOMIC_ACQ_REL);
+        sv->share.hdr = h;
+    }
+    sv->share.bytes = bytes;
+    sv->share.ent = (MailEntry*)(sv->share.hdr + 1);
+    sv->share.nranks = nranks;
+    sv->share.rank = rank;
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_share_emulated(tk_solver* sv, int nranks, int rank, const double* results) { TK_API_BEGIN
+    if (!sv || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !results))
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_share_emulated: bad argument");
+    share_close(sv->share);
+    if (nranks == 1) return TK_OK;
+    sv->share.table.assign(results, results + (size_t)sv->kmax * RES_N);
+    sv->share.nranks = nranks;
+    sv->share.rank = rank;
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_results(tk_solver* sv, double* out) { TK_API_BEGIN
+    if (!sv || !out) return tk_fail_internal(TK_ERR_ARG, "tk_solver_results: bad argument");
+    memcpy(out, sv->results.data(), sv->results.size() * sizeof(double));
+    return TK_OK;
+    TK_API_END
+}
+
+tk_status tk_solver_evaluate_shared(tk_solver* sv, int k, double* out4) { TK_API_BEGIN
+    if (!sv || !out4 || k < 2 || k > sv->kmax || sv->rank[k - 1] < 1)
+        return tk_fail_internal(TK_ERR_ARG, "tk_solver_evaluate_shared: bad argument");
+    Share& sh = sv->share;
+    if (!sh.on()) return tk_solver_evaluate(sv, k, out4);
+    if (k <= sh.last_k) ++sh.gen;   // a new loop (every rank restarts at the same k)
+    sh.last_k = k;
+    IterResult r;
+    if (sh.owner(k)) {
+        evaluate(sv, k, sv->last, sv->ws);
+        mail_post(sv, sv->last);
+        r = sv->last;
+    } else {
+        tk_status st = mail_take(sv, k, r, std::chrono::steady_clock::now());
+        if (st) return st;
+    }
+    out4[0] = r.r_comp;
+    out4[1] = r.r_norm;
+    out4[2] = r.rel;
+    out4[3] = r.orth;
+    if (r.status == TK_ERR_STATE) return tk_fail_internal(TK_ERR_STATE, "compressed solve failed (eigen / expm)");
+    return r.status;
+    TK_API_END
+}
+
 tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, int depth, int nthreads,
                         double* relres, double* projres, double* orth, int* k_end, int* outcome) { TK_API_BEGIN
     if (!sv || !dc || !relres || !projres || !orth || !k_end || !outcome || kfirst < 2)
@@ -533,13 +781,25 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         }
     // every rank must issue the same sequence of steps and record reads (the records
     // all-reduces follow it, tk_xsched.h): agree the worker count and depth (max over ranks)
-    int agreed[2] = {std::max(1, std::min(nthreads, 64)), depth};
+    // ... and whether the evaluations are split over the ranks: on only if EVERY rank has the
+    // mailbox (max of the flag = 1 and max of its negation = 0), so no rank waits for results
+    // a rank without one would never post
+    Share& sh = sv->share;
+    const int son = sh.on() ? 1 : 0;
+    int agreed[4] = {std::max(1, std::min(nthreads, 64)), depth, son, -son};
     {
-        tk_status st0 = tk_decomp_agree(dc, agreed, 2);
+        tk_status st0 = tk_decomp_agree(dc, agreed, 4);
         if (st0) return st0;
     }
     const int P = agreed[0];
     depth = std::max(agreed[1], P + 1);
+    const bool split = agreed[2] == 1 && agreed[3] == -1;
+    ++sh.gen;                        // (every rank counts its runs alike)
+    sh.last_k = 1 << 30;
+    // dispatch window: P evaluations in flight per rank; split, each rank owns 1 of NR
+    const int NR = split ? sh.nranks : 1;
+    const int W = P * NR;
+    std::fill(sv->results.begin(), sv->results.end(), NAN);
     *outcome = 0;
     *k_end = klast;
     std::vector<double> rec((size_t)sv->d * sv->m);
@@ -585,6 +845,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
         std::lock_guard<std::mutex> lk(pool.mu);
         for (auto& x : pool.done) x = 0;
     }
+    typedef std::chrono::steady_clock clk_t;
     // the last two iterations run when every other evaluation is done or nearly so: their
     // data-parallel parts may be split over the helper threads (Work::nthreads, Work::par;
     // bitwise the same), which spin from the dispatch of iteration klast-2 on
@@ -598,6 +859,11 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     } hot_off{hp};
     // per worker: the iteration submitted and not yet consumed (quiesce waits for its result)
     std::vector<int> inflight(workers.size(), 0);
+    // per iteration: the worker evaluating it here (-1: another rank's, read from the mailbox),
+    // and when its record was applied here (emulation releases the owner's result from then)
+    std::vector<int> wmap(kmax + 2, -1);
+    std::vector<clk_t::time_point> t_disp(kmax + 2);
+    int nsub = 0;
     auto submit = [&](int w, int k) {
         {
             std::lock_guard<std::mutex> lk(pool.mu);
@@ -655,7 +921,7 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     std::vector<double> tr_e0(kmax + 2, -1.0), tr_e1(kmax + 2, -1.0);
     for (int k = kfirst; k <= klast; ++k) {
         // keep P evaluations in flight: records of step k_dispatch-1, applied in order
-        while (k_dispatch <= klast && k_dispatch < k + P) {
+        while (k_dispatch <= klast && k_dispatch < k + W) {
             lap(t_wait);
             err = tk_decomp_records(dc, k_dispatch, k_dispatch + 1, rec.data());
             lap(t_rec);
@@ -664,8 +930,15 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             lap(t_issue);
             if (err) break;
             apply_record(sv, k_dispatch - 1, rec.data());
-            if (etr) tr_rec[k_dispatch] = since(clk::now());
-            submit((k_dispatch - kfirst) % P, k_dispatch);
+            t_disp[k_dispatch] = clk::now();
+            if (etr) tr_rec[k_dispatch] = since(t_disp[k_dispatch]);
+            if (!split || sh.owner(k_dispatch)) {
+                // owned iterations round-robin over the workers: at most P of them lie in a
+                // window of W = P * NR, so a worker's previous one has been consumed
+                const int w = nsub++ % P;
+                wmap[k_dispatch] = w;
+                submit(w, k_dispatch);
+            }
             ++k_dispatch;
             lap(t_apply);
         }
@@ -674,10 +947,26 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             err = read_gram();
             if (err) break;
         }
-        Worker& wk = *workers[(k - kfirst) % P];
-        wait_done((k - kfirst) % P, k);
+        IterResult other;
+        IterResult* rp = &other;
+        if (wmap[k] >= 0) {
+            wait_done(wmap[k], k);
+            rp = &workers[wmap[k]]->res;
+        } else {
+            err = mail_take(sv, k, other, t_disp[k]);
+            if (err) break;
+        }
         lap(t_wait);
-        IterResult& r = wk.res;
+        IterResult& r = *rp;
+        {
+            double* q = &sv->results[(size_t)(k - 1) * RES_N];
+            q[RES_RC] = r.r_comp;
+            q[RES_RN] = r.r_norm;
+            q[RES_REL] = r.rel;
+            q[RES_ORTH] = r.orth;
+            q[RES_ST] = r.status;
+            q[RES_US] = (wmap[k] >= 0 && r.t0 >= 0) ? 1e6 * (r.t1 - r.t0) : -1.0;
+        }
         if (etr) {
             tr_cons[k] = since(clk::now());
             tr_e0[k] = r.t0 >= 0 ? std::chrono::duration<double, std::micro>(std::chrono::duration<double>(r.t0)).count() : -1;
@@ -709,6 +998,9 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
     if (!err && !gram_loss.empty())
         for (int k = kfirst; k <= std::min(*k_end, gram_k); ++k) orth[k - 1] = gram_loss[k - 1];
     quiesce();
+    // converged on an iteration another rank evaluated: its y (lambda, Y) is needed here too
+    // (basis_tensor_mul! of this rank's factors) -- evaluate it locally, bitwise the owner's
+    if (!err && *outcome == 1 && sv->last.Y.empty()) evaluate(sv, *k_end, sv->last, sv->ws);
     const auto t_quiet = clk::now();
     if (etr) {
         if (FILE* f = fopen(etr, "w")) {

@@ -18,7 +18,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <ctype.h>
+#include <unistd.h>
+
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/tk.h"
@@ -45,8 +49,10 @@ struct tk_decomp {
     int agree_idx = 0;
 };
 
-// the job's agreement: every rank's submissions, max taken when a rank asks
+// the job's agreement: every rank's submissions (tk_solver_run's: worker count, depth, the
+// evaluation-split flag and its negation), max taken when a rank asks
 static std::vector<std::vector<int>> g_sub;   // [rank][value]
+static std::vector<int> g_group;              // [rank] TKHIP_XCH_GROUP
 static int g_rank = 0;
 // XSCHED_SIM_LOCAL=1 (negative control): no agreement -- each rank keeps its own worker
 // count, depth and group size, as before tk_decomp_agree / the create preflight existed
@@ -156,11 +162,13 @@ static void flush(tk_decomp* dc) {
 
 struct RankCfg {
     int kind, threads, depth, group;
+    int split = 0;   // 1: tk_solver_share over the job's ranks (threads, real mailbox)
 };
+static std::string g_key;   // the job's mailbox key
 
 // one rank's whole call sequence: the Python driver's init + step 0 (records out), the
 // native loop, then basis_mul / flush on convergence (tkamd/solver.py)
-static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, double tol) {
+static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, double tol, int myrank, int nranks) {
     tk_decomp dc;
     dc.kind = rc.kind;
     dc.kmax = kmax;
@@ -169,7 +177,7 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
     dc.xs.group = rc.group;
     // tk_decomp_create's preflight: the group size is the max over the ranks
     if (!g_local)
-        for (const auto& r : g_sub) dc.xs.group = std::max(dc.xs.group, r[2]);
+        for (int g : g_group) dc.xs.group = std::max(dc.xs.group, g);
     std::vector<double> rec((size_t)d * dc.m);
     tk_decomp_init(&dc, rec.data());
     tk_decomp_step(&dc, 0, rec.data());
@@ -180,6 +188,17 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
         fprintf(stderr, "tk_solver_create: %s\n", g_err);
         exit(2);
     }
+    if (rc.split == 1 && tk_solver_share(sv, g_key.c_str(), nranks, myrank)) {
+        fprintf(stderr, "tk_solver_share: %s\n", g_err);
+        exit(2);
+    }
+    // split = 2: this rank alone has a results source (an emulation table); the run's
+    // agreement must then turn the split off on every rank
+    std::vector<double> table((size_t)kmax * 6, 0.0);
+    if (rc.split == 2 && tk_solver_share_emulated(sv, nranks, myrank, table.data())) {
+        fprintf(stderr, "tk_solver_share_emulated: %s\n", g_err);
+        exit(2);
+    }
     std::vector<double> relres(kmax), proj(kmax), orth(kmax);
     int k_end = 0, outcome = 0;
     tk_status st = tk_solver_run(sv, &dc, tol, 2, rc.depth, rc.threads, relres.data(), proj.data(), orth.data(),
@@ -187,6 +206,13 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
     if (st) {
         fprintf(stderr, "tk_solver_run: %d %s\n", st, g_err);
         exit(2);
+    }
+    char rb[96];
+    snprintf(rb, sizeof rb, "relres[%d]=%.17g", k_end - 1, relres[k_end - 1]);
+    std::vector<double> lam(1), Y((size_t)d * k_end);
+    if (outcome == 1 && tk_solver_solution(sv, k_end, lam.data(), Y.data())) {   // (every rank: its y)
+        fprintf(stderr, "rank %d: tk_solver_solution: %s\n", myrank, g_err);
+        exit(5);
     }
     tk_solver_destroy(sv);
     if (outcome == 1) flush(&dc);   // basis_mul's flush of the pending column
@@ -206,16 +232,38 @@ static std::vector<std::string> run_rank(const RankCfg& rc, int kmax, int d, dou
     char b[64];
     snprintf(b, sizeof b, "end k=%d outcome=%d", k_end, outcome);
     dc.log.push_back(b);
+    dc.log.push_back(rb);
     return dc.log;
 }
 
 static int run_job(const char* name, const std::vector<RankCfg>& ranks, int kmax, int d, double tol) {
     g_sub.clear();
-    for (const RankCfg& r : ranks) g_sub.push_back({r.threads, r.depth, r.group});
-    std::vector<std::vector<std::string>> logs;
-    for (size_t i = 0; i < ranks.size(); ++i) {
-        g_rank = (int)i;
-        logs.push_back(run_rank(ranks[i], kmax, d, tol));
+    g_group.clear();
+    bool split = false;
+    for (const RankCfg& r : ranks) {
+        const int on = r.split ? 1 : 0;
+        g_sub.push_back({r.threads, r.depth, on, -on});
+        g_group.push_back(r.group);
+        split = split || r.split == 1;
+    }
+    const int nr = (int)ranks.size();
+    std::vector<std::vector<std::string>> logs(nr);
+    if (!split) {
+        for (int i = 0; i < nr; ++i) {
+            g_rank = i;
+            logs[i] = run_rank(ranks[i], kmax, d, tol, i, nr);
+        }
+    } else {
+        // the evaluation split: ranks wait for each other's results, so they run concurrently
+        // (each on its own thread with its own stand-in decomposition), through the real mailbox
+        char key[64];
+        snprintf(key, sizeof key, "xsim_%d_%s", (int)getpid(), name);
+        for (char* p = key; *p; ++p)
+            if (!isalnum((unsigned char)*p)) *p = '_';
+        g_key = key;
+        std::vector<std::thread> th;
+        for (int i = 0; i < nr; ++i) th.emplace_back([&, i] { logs[i] = run_rank(ranks[i], kmax, d, tol, i, nr); });
+        for (auto& t : th) t.join();
     }
     bool same = true;
     for (size_t i = 1; i < logs.size(); ++i) same = same && logs[i] == logs[0];
@@ -249,6 +297,18 @@ int main() {
     bad += run_job("mixed8", {{ONESWEEP, 8, 2, 4}, {ONESWEEP, 8, 2, 4}, {CGS2, 8, 2, 4}, {EMPTY, 8, 2, 4},
                               {ONESWEEP, 1, 9, 4}, {CGS2, 2, 2, 4}, {EMPTY, 5, 2, 2}, {ONESWEEP, 3, 4, 7}},
                    K, d, 0.0);
+    // the evaluation split (tk_solver_share): every rank evaluates 1 / nranks of the
+    // iterations and reads the others' from the mailbox -- same all-reduces, same outcome
+    if (!g_local) {
+        bad += run_job("split2", {{ONESWEEP, 4, 2, 4, 1}, {ONESWEEP, 2, 3, 4, 1}}, K, d, 0.0);
+        bad += run_job("split-converged", {{ONESWEEP, 4, 2, 4, 1}, {EMPTY, 8, 3, 4, 1}, {CGS2, 1, 2, 16, 1}}, K, d, 1.0);
+        bad += run_job("split8", {{ONESWEEP, 8, 2, 4, 1}, {ONESWEEP, 8, 2, 4, 1}, {CGS2, 8, 2, 4, 1}, {EMPTY, 8, 2, 4, 1},
+                                  {ONESWEEP, 1, 9, 4, 1}, {CGS2, 2, 2, 4, 1}, {EMPTY, 5, 2, 2, 1}, {ONESWEEP, 3, 4, 7, 1}},
+                       K, d, 0.0);
+        // one rank with a results source, one without: nobody splits (the agreed flag), the
+        // same sequence
+        bad += run_job("split-partial", {{ONESWEEP, 4, 2, 4, 0}, {ONESWEEP, 4, 2, 4, 2}}, K, d, 0.0);
+    }
     printf("RESULT %s\n", bad ? "MISMATCH" : "OK");
     return bad ? 1 : 0;
 }

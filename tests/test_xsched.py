@@ -38,7 +38,7 @@ def _run(sim, local):
 def test_every_rank_issues_the_same_allreduces(sim):
     p, jobs = _run(sim, local=False)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert len(jobs) == 7
+    assert len(jobs) == 11
     for line in jobs:
         assert "identical=1" in line, line
     # the default group of 4 batches the step slots once the issue depth covers a group
@@ -46,7 +46,7 @@ def test_every_rank_issues_the_same_allreduces(sim):
     assert "[2,5]x3520" in first and "[46,49]x3520" in first, first
     # converged job: the flush slot (kmax + 1) goes out once, after every issued step's slot
     conv = [l for l in jobs if l.startswith("JOB converged")][0]
-    assert conv.split("first=")[1].split()[-4] == "[51,51]x880", conv
+    assert conv.split("first=")[1].split()[-5] == "[51,51]x880", conv
 
 
 def test_without_agreement_ranks_diverge(sim):
@@ -55,3 +55,24 @@ def test_without_agreement_ranks_diverge(sim):
     p, jobs = _run(sim, local=True)
     assert p.returncode == 1
     assert any("identical=0" in l for l in jobs)
+
+
+def test_evaluation_split_over_ranks(sim):
+    """tk_solver_share: ranks running concurrently, each evaluating the
+    iterations k = rank (mod nranks) and reading the others' results from the real
+    shared-memory mailbox, issue the same all-reduces and end at the same iteration with the
+    same outcome and residual (the log's last entries); a rank that converges on another
+    rank's iteration still returns its y (tk_solver_solution).  With one rank lacking a
+    results source the run's agreement turns the split off everywhere.  No file is left in
+    /dev/shm."""
+    before = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
+    p, jobs = _run(sim, local=False)
+    assert p.returncode == 0, p.stdout + p.stderr
+    split = [l for l in jobs if l.startswith("JOB split")]
+    assert len(split) == 4
+    for line in split:
+        assert "identical=1" in line, line
+    conv = [l for l in split if l.startswith("JOB split-converged")][0]
+    assert "outcome=1" in conv
+    after = set(os.listdir("/dev/shm")) if os.path.isdir("/dev/shm") else set()
+    assert not [f for f in after - before if f.startswith("tkhip_ev_")]
