@@ -257,7 +257,7 @@ def main():
             b_ = np.random.default_rng(1000 + s_).random(n)
             allb.append(b_ / np.linalg.norm(b_))
         kron = tkamd.KroneckerMatrix(inst, [csc] * d, cls)
-        overlay = ref_relres = None
+        overlay = ref_relres = eval_overlay = None
         if args.emulate_ranks > 1 and world == 1:
             # the other ranks' factors: their records from a full run on this GPU (the same
             # records an N-rank job all-reduces), and the N = 1 trajectory to compare with
@@ -270,12 +270,17 @@ def main():
             conv1 = tkamd.ConvergenceData(K)
             tkamd.tensorkrylov(conv1, kron, allb, 1e-9, K, method, ctx=ctx)
             ref_relres = conv1.relative_residual_norm.copy()
+            # this rank evaluates only the iterations it owns (k % N == rank, the evaluation
+            # split of an N-rank job); the others' results come from the full run's table
+            if os.environ.get("TKHIP_EVAL_SPLIT", "1") != "0":
+                eval_overlay = getattr(conv1, "native_results", None)
         samples = []
         for _ in range(max(1, args.e2e_reps)):
             conv = tkamd.ConvergenceData(K)
             barrier()
             te = time.perf_counter()
-            tkamd.tensorkrylov(conv, kron, allb, 1e-9, K, method, ctx=ctx, partition=part, overlay=overlay)
+            tkamd.tensorkrylov(conv, kron, allb, 1e-9, K, method, ctx=ctx, partition=part, overlay=overlay,
+                               eval_overlay=eval_overlay)
             barrier()
             te = time.perf_counter() - te
             loop = conv.timing.get("loop_s", te)
@@ -288,7 +293,14 @@ def main():
         # the median solve by loop time (its phases and trajectory are reported)
         samples.sort(key=lambda x: x[0])
         loop, te, conv = samples[len(samples) // 2]
-        e2e = {"iterations_s": round(max(conv.niterations - 1, 1) / loop, 2),
+        e2e_rate = max(conv.niterations - 1, 1) / loop
+        # like for like: the device rate of the loop's own work -- the K steps of a sweep
+        # without the end-of-solve V*Y and Gram (a solve that does not converge runs neither)
+        loop_dev = (K * sweep_cnt) / (sweep_ms / 1e3) if sweep_cnt else None
+        e2e = {"iterations_s": round(e2e_rate, 2),
+               "device_steps_only_iterations_s": round(loop_dev, 2) if loop_dev else None,
+               "vs_device_steps_only": round(e2e_rate / loop_dev, 4) if loop_dev else None,
+               "eval_split": getattr(conv, "eval_split", None),
                "solves": len(samples),
                "iterations_s_all": [round(max(c_.niterations - 1, 1) / l_, 2) for l_, _, c_ in samples],
                "iterations": int(conv.niterations),
@@ -355,8 +367,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
             "higher_is_better": True,
-            **({"emulated": "rank 0 of %d on one GPU: per-rank time of an N-GPU run, NOT a "
-                            "whole-job number" % args.emulate_ranks} if args.emulate_ranks else {}),
+            **({"emulated": "rank %d of %d on one GPU: per-rank time of an N-GPU run, NOT a "
+                            "whole-job number" % (args.emulate_rank, args.emulate_ranks)} if args.emulate_ranks else {}),
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",

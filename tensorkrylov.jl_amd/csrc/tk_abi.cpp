@@ -1394,6 +1394,17 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
     } while (0);                           \
     LAUNCHCHK(name)
 
+// TKHIP_D1_CACHE_MB: the per-step working set (MiB) up to which the one-sweep Arnoldi step
+// loads the basis with the default cache policy instead of nt (0: always nt).  The Infinity
+// Cache is 256 MiB; a line stays resident while everything touched between two uses fits
+static double d1_cache_bytes() {
+    static const double v = [] {
+        const char* e = getenv("TKHIP_D1_CACHE_MB");
+        return (e ? std::max(0.0, atof(e)) : 224.0) * 1048576.0;
+    }();
+    return v;
+}
+
 // Step j's record is enqueued on this rank (its k_post, or the bookkeeping block of the
 // next k_arn_d1): count its signal and note its host sequence number.  Local only.
 static void complete_step(tk_decomp* dc, int j, unsigned long long seqj) {
@@ -1558,6 +1569,11 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             tk_status st2 = bk_flush(dc);
             if (st2) return st2;
         }
+        // the basis rows through the caches while this rank's per-step working set (every
+        // local factor's V[:, 0..j) and u in / out, v_j) fits the Infinity Cache: the next step
+        // then re-reads them from there (emulated N = 8, C2: +3..5 %); streamed with nt beyond
+        // (N = 1, C2: -4.5 % with the default policy; profiles/r05/vload_policy_ab.txt)
+        const bool vcache = (double)nf * 8.0 * (double)dc->ld * (double)(j + 3) <= d1_cache_bytes();
         if (grouped) {
             // each factor group in its own launches on its own stream (the bookkeeping blocks
             // of a group's launch serve that group's factors: host-mirror words offset by g0)
@@ -1570,7 +1586,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                 {
                     Timer tm_(c, TCLS_PASS1, 2, sg);
-                    launch_arn_d1(dc->df + g0, ng, a, bg, dc->npd, dc->any_gram, sg);
+                    launch_arn_d1(dc->df + g0, ng, a, bg, dc->npd, dc->any_gram, vcache, sg);
                 }
                 LAUNCHCHK("arn_d1");
                 if (!(dc->skip_mask & 1)) {
@@ -1580,7 +1596,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 LAUNCHCHK("reduce");
             }
         } else {
-            RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, s), "arn_d1");
+            RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, vcache, s), "arn_d1");
             // (its last block per factor also evaluates the next step's scalars)
             if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
         }

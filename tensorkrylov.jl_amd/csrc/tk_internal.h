@@ -143,7 +143,8 @@ void launch_arn_a1_fused(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, hipStream_t s);
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, bool vcache,
+                   hipStream_t s);
 void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 // the gram-free one-sweep Lanczos step (k_lan_1w; npd = the largest DFac::nwl); b.j >= 0: the
 // previous step's record mirror + signal ride in 8 leading blocks

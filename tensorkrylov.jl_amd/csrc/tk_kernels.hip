@@ -84,8 +84,9 @@ __device__ __forceinline__ double bld(rsrc_t r, uint32_t off) {
 }
 
 typedef double d2_t __attribute__((ext_vector_type(2)));
+template <int AUX = TK_V_AUX>
 __device__ __forceinline__ d2_t bld2(rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(d2_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, TK_V_AUX));
+    return __builtin_bit_cast(d2_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX));
 }
 // Paired-column tile layout: element offset of (row t, column c) inside a tile, byte
 // offset of column c relative to thread t's pair base (t*16), tile stride, and the
@@ -274,13 +275,15 @@ struct Row {
     // column checks, and `last` is one of their columns.
     // loadm for an even nc: whole pairs only, no selects on the loaded values (a uniform
     // select there made the compiler wait for the row before its next loads); `last` unset
-    template <int PLO = 0>   // pairs below PLO are not loaded (k_arn_d1 keeps them in LDS)
+    // AUX: the load's cache policy (k_arn_d1: nt, or the default policy while the rank's
+    // per-step working set fits the Infinity Cache)
+    template <int PLO = 0, int AUX = TK_V_AUX>   // pairs below PLO are not loaded (k_arn_d1 keeps them in LDS)
     __device__ __forceinline__ void loadm_even(rsrc_t basis, uint32_t toff, int nc) {
         constexpr int P0 = MAXC / 2 - 4;
 #pragma unroll
         for (int p = PLO; p < MAXC / 2; ++p) {
             const uint32_t off = (p < P0 || 2 * p < nc) ? toff + (uint32_t)p * (TPB * 16) : 0x80000000u;
-            const d2_t x = bld2(basis, off);
+            const d2_t x = bld2<AUX>(basis, off);
             v[2 * p] = x.x;
             v[2 * p + 1] = x.y;
         }
@@ -992,7 +995,7 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #endif
 __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds);
 __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent = false);
-template <int MAXC, int FMT>
+template <int MAXC, int FMT, bool VC>
 #ifndef TK_D1_OCCT
 #define TK_D1_OCCT 2
 #endif
@@ -1110,7 +1113,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                     tv, (__attribute__((address_space(3))) void*)(vl + p * TPB + (t & ~63)), 16,
                     toff + (uint32_t)p * (TPB * 16), 0, 0, 2);
         }
-        R.template loadm_even<LC / 2>(tv, toff, jl);
+        // VC: the basis row through the caches (default policy) -- the launcher's choice when
+        // this rank's per-step working set fits the 256 MiB Infinity Cache, so the next step
+        // re-reads it from there; nt otherwise (streamed once, never re-read in time)
+        R.template loadm_even<LC / 2, VC ? 0 : 2>(tv, toff, jl);
         // (both loads issued before the patch below waits for the row)
         const double up = inb ? ld(Uin, r) : 0.0;
         const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
@@ -2960,7 +2966,8 @@ void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
         else hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value, false>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
     });
 }
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, hipStream_t s) {
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, bool vcache,
+                   hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
@@ -2971,8 +2978,12 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     const int gx = TK_D1_ONEWIN ? (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
     with_band_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
-            hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value>), dim3(gx, nf), dim3(TPB),
-                               lds, s, F, a, b);
+            if (vcache)
+                hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value, true>), dim3(gx, nf), dim3(TPB),
+                                   lds, s, F, a, b);
+            else
+                hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value, false>), dim3(gx, nf), dim3(TPB),
+                                   lds, s, F, a, b);
         });
     });
 }

@@ -87,6 +87,10 @@ def lib():
         "tk_solver_state": (I, [P, DP, DP, DP]),
         "tk_solver_run": (I, [P, P, ctypes.c_double, I, I, I, DP, DP, DP, ctypes.POINTER(I), ctypes.POINTER(I)]),
         "tk_solver_prepare": (I, [P, I]),
+        "tk_solver_share": (I, [P, ctypes.c_char_p, I, I]),
+        "tk_solver_share_emulated": (I, [P, I, I, DP]),
+        "tk_solver_results": (I, [P, DP]),
+        "tk_solver_evaluate_shared": (I, [P, I, DP]),
         "tk_orthogonality_losses": (I, [I, DP, DP]),
     }
     for name, (res, args) in sigs.items():
@@ -109,7 +113,8 @@ EXPORTS = ("tk_last_error", "tk_version", "tk_ctx_create", "tk_ctx_destroy", "tk
            "tk_decomp_get_basis", "tk_decomp_basis_mul", "tk_timing_enable", "tk_timing_read",
            "tk_compressed_solve", "tk_residualnorm", "tk_solver_create", "tk_solver_destroy", "tk_solver_overlay",
            "tk_solver_apply", "tk_solver_evaluate", "tk_solver_rank", "tk_solver_solution", "tk_solver_state",
-           "tk_solver_run", "tk_solver_prepare", "tk_orthogonality_losses")
+           "tk_solver_run", "tk_solver_prepare", "tk_solver_share", "tk_solver_share_emulated", "tk_solver_results",
+           "tk_solver_evaluate_shared", "tk_orthogonality_losses")
 
 TK_BREAKDOWN = 7
 

@@ -287,6 +287,7 @@ class NativeSolver:
                                          rank.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                                          L.dptr(tables.alpha), L.dptr(tables.omega), ctypes.byref(h)))
         self.h = h
+        self.split = None          # (nranks, rank) once the evaluations are split (share)
 
     def overlay(self, first, nf, records):
         """Emulation only: rows of factors outside [first, first+nf) come from `records`
@@ -324,6 +325,42 @@ class NativeSolver:
         self._L.check(self._L.lib().tk_solver_state(self.h, self._L.dptr(H), self._L.dptr(bt),
                                                     self._L.dptr(G)))
         return H, bt, G
+
+    def share(self, key, nranks, rank):
+        """Split the evaluations over the ranks of this node (tk_solver_share): rank
+        k % nranks evaluates iteration k, the others read its result from a shared-memory
+        mailbox.  Collective (same key on every rank)."""
+        self._L.check(self._L.lib().tk_solver_share(self.h, key.encode(), int(nranks), int(rank)))
+        self.split = (int(nranks), int(rank)) if nranks > 1 else None
+
+    def share_emulated(self, nranks, rank, results):
+        """Emulation (bench.py --emulate-ranks): the split on one rank, the other ranks' results
+        from a full run's `results` ([kmax][6], results())."""
+        self._tab = np.ascontiguousarray(results, dtype=np.float64)
+        assert self._tab.shape == (self.kmax, 6)
+        self._L.check(self._L.lib().tk_solver_share_emulated(self.h, int(nranks), int(rank), self._L.dptr(self._tab)))
+        self.split = (int(nranks), int(rank)) if nranks > 1 else None
+
+    def evaluate_shared(self, k):
+        """evaluate(k) under the split: owner evaluates and posts, the others read."""
+        out = np.zeros(4)
+        st = self._L.lib().tk_solver_evaluate_shared(self.h, int(k), self._L.dptr(out))
+        if st == self._L.TK_BREAKDOWN:
+            raise CompressedNormBreakdown(out[0])
+        self._L.check(st)
+        return tuple(float(x) for x in out)
+
+    def owns(self, k):
+        sp = getattr(self, "split", None)
+        return sp is None or k % sp[0] == sp[1]
+
+    def results(self):
+        """Per iteration of the last run: [kmax][6] = r_comp, r_norm, relres, orthogonality,
+        status, evaluation us on this rank (-1: evaluated by another rank); NaN rows where the
+        run consumed nothing (tk_solver_results)."""
+        out = np.zeros((self.kmax, 6))
+        self._L.check(self._L.lib().tk_solver_results(self.h, self._L.dptr(out)))
+        return out
 
     def prepare(self, nthreads):
         """Start the evaluation threads now (setup), not inside the loop (tk_solver_prepare)."""

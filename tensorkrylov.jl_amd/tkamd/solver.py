@@ -31,7 +31,7 @@ def _native_threads():
 
 def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbose=False,
                  backend=None, keep_decomposition=False, pipelined=True, depth=2, native=True,
-                 threads=None, overlay=None):
+                 threads=None, overlay=None, eval_overlay=None):
     """tensorkrylov!(convergence_data, A, b, tol, nmax, orthonormalization_type).
     Returns the approximate solution as a KruskalTensor of the LOCAL factors
     (x_s = V_s y_s; with a term-splitting Partition only this rank's slice x.terms of the
@@ -50,7 +50,16 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
     threads, consumed in order -- the same iterates).  native=False keeps the Python loop
     below (the mirror of the reference's driver, used to cross-check the native one).
     overlay (diagnostic, native only): a full run's records [nmax+2][d][m]; the records of
-    factors this rank does not own are taken from it (bench.py --emulate-ranks)."""
+    factors this rank does not own are taken from it (bench.py --emulate-ranks).
+    eval_overlay (diagnostic, with overlay): a full run's per-iteration results
+    (conv.native_results) -- this rank then evaluates only its share of the iterations
+    (k % N == rank) and takes the others' from the table, each released no earlier than the
+    owner would have had it (tk_solver_share_emulated).
+
+    With several ranks (partition) on one node the native solver splits the evaluations over
+    the ranks (tk_solver_share, a shared-memory mailbox; TKHIP_EVAL_SPLIT=0 turns it off):
+    every rank still applies every record, so each iterate is bitwise what it would have
+    computed itself."""
     if isinstance(method, str):
         method = METHODS[method]
     d = len(A)
@@ -74,6 +83,11 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             try:
                 if overlay is not None:
                     sv.overlay(td.part.first, td.part.nf, overlay)
+                    if eval_overlay is not None and td.part.nranks > 1:
+                        sv.share_emulated(td.part.nranks, td.part.rank, eval_overlay)
+                elif _split_wanted(td.part):
+                    sv.share(_share_key(td), td.part.nranks, td.part.rank)
+                conv.eval_split = sv.split
                 for j, rec in td.first_records:
                     sv.apply(j, rec)
                 t_loop = time.perf_counter()
@@ -139,6 +153,31 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
             conv.decomposition = td
         else:
             td.close()
+
+
+def _split_wanted(part):
+    """Evaluation split over the ranks (tk_solver_share): several ranks, all on this node
+    (the mailbox is node-local shared memory; torch.distributed.run sets LOCAL_WORLD_SIZE),
+    not turned off by TKHIP_EVAL_SPLIT=0.  Every rank decides the same way; if a rank still
+    ends up without a mailbox, tk_solver_run's agreement turns the split off everywhere."""
+    import os
+    if part.nranks <= 1 or os.environ.get("TKHIP_EVAL_SPLIT", "1") == "0":
+        return False
+    lw, w = os.environ.get("LOCAL_WORLD_SIZE"), os.environ.get("WORLD_SIZE")
+    return lw is None or w is None or lw == w
+
+
+def _share_key(td):
+    """A job-unique mailbox key every rank agrees on: rank 0 draws it, one host all-reduce
+    (setup, not the loop) hands it to the others."""
+    import os
+    part = td.part
+    v = np.zeros(2)
+    if part.rank == 0:
+        v[0] = float(int.from_bytes(os.urandom(6), "little"))
+        v[1] = float(os.getpid())
+    v = (td.ctx if td.ctx is not None else td.dev).allreduce_host(v)
+    return "%x_%x_%d" % (int(v[0]), int(v[1]), part.nranks)
 
 
 def _gram_deferred(td):
@@ -219,6 +258,8 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
         conv.orthogonality_data[1:k_end] = orth[1:k_end]
     else:
         outcome, k_end = 0, nmax
+        # (split over the ranks: the owner of k evaluates it, the others read its result)
+        evaluate = sv.evaluate_shared if getattr(sv, "split", None) else sv.evaluate
         for k in range(2, nmax + 1):
             if tables.rank[k - 1] < 1:
                 k_end = k - 1
@@ -226,7 +267,7 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
             td.orthonormalize(k)                                    # :66
             sv.apply(k - 1, td._last_rec)
             try:
-                r_comp, _, rel_k, orth_k = sv.evaluate(k)           # :68-103
+                r_comp, _, rel_k, orth_k = evaluate(k)              # :68-103
             except CompressedNormBreakdown:
                 outcome, k_end = 2, k - 1
                 break
@@ -238,10 +279,14 @@ def _native_loop(conv, td, sv, tables, tol, nmax, verbose, pipelined, depth, thr
                 break
     x = None
     if outcome == 1:                                                # :108-118
+        if not (device and pipelined) and not sv.owns(k_end):
+            sv.evaluate(k_end)      # another rank evaluated it: this rank's y, bitwise the same
         lam, Ys = sv.solution(k_end)
         x = _solution(td, k_end, lam, Ys)
     _fill_deferred_orthogonality(conv, td, k_end, conv.orthogonality_data if device and pipelined else None)
     conv.timing["loop_s"] = time.perf_counter() - t_loop
+    if device and pipelined:
+        conv.native_results = sv.results()   # (bench.py --emulate-ranks: the eval_overlay table)
     # the host mirror of H, b~ and factor 1's Gram rows (principal_minors readers)
     H, bt, G = sv.state()
     td.H[...] = H

@@ -37,6 +37,7 @@ def main():
     res = {"rank": rank, "world": world, "local": list(part.local()),
            "relres": conv.relative_residual_norm.tolist(), "proj": conv.projected_residual_norm.tolist(),
            "orth": conv.orthogonality_data.tolist(), "niter": conv.niterations,
+           "eval_split": getattr(conv, "eval_split", None),
            "x_factors": None if x is None else x.factors,
            "x_terms": None if x is None else list(x.terms),
            "x_lam": None if x is None else x.lam.tolist(),

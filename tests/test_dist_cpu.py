@@ -63,7 +63,10 @@ def test_partitioned_run_equals_single_process(tmp_path, world, method, d, K):
     ref = _single(method, d, K)
     owned = sorted(s for rr in res for s in rr["local"])
     assert owned == list(range(d))
-    for rr in res:                       # every rank evaluates the same compressed residual
+    for rr in res:                       # every rank ends with the same compressed residuals
+        # (each rank evaluates the iterations k = rank mod world and reads the others' from the
+        # shared-memory mailbox: tk_solver_share)
+        assert rr["eval_split"] == [world, rr["rank"]]
         assert rr["niter"] == ref.niterations
         assert np.array_equal(rr["relres"], ref.relative_residual_norm)
         assert np.array_equal(rr["proj"], ref.projected_residual_norm)
