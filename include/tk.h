@@ -148,6 +148,13 @@ int tk_decomp_matrix_reads(tk_decomp* dc);
  * rank issues the same sequence of steps, record reads and therefore all-reduces. */
 tk_status tk_decomp_agree(tk_decomp* dc, int* vals, int count);
 
+/* The one-sweep steps' reduce hand-off: 0 = relaxed agent-scope atomics
+ * (measured correct on gfx950, and confirmed by a self-check against the memory-model form at
+ * the process's first tk_decomp_create), 1 = the HIP memory model's release/acquire form (kept
+ * when the self-check finds any difference or cannot run; TKHIP_RED_MM=0/1 forces a form),
+ * -1 = not settled yet (no decomposition created). */
+int tk_reduce_handoff(void);
+
 /* Multi-rank waits (the records exchange, tk_comm_allreduce_host, tk_ctx_sync, destroy) are
  * bounded by TKHIP_WAIT_S seconds (default 120): on expiry the call returns TK_ERR_RCCL naming
  * the record slot / step it waited for and RCCL's asynchronous error state, and the context

@@ -288,6 +288,7 @@ tk_status tk_ctx_create(int device, tk_ctx** out) { TK_API_BEGIN
     TK_API_END
 }
 
+
 static void ctx_release(tk_ctx* c) {
     if (--c->refs > 0) return;
     hipSetDevice(c->device);
@@ -828,10 +829,103 @@ static void free_decomp(tk_decomp* dc) {
     delete dc;
 }
 
+// ------------------------------------------------------------------ reduce hand-off self-check
+// k_reduce256 hands a one-sweep step's reduced values to the block that evaluates the next
+// step's scalars through agent-scope relaxed atomics -- correct on gfx950 by measurement
+// (/opt/skills/guides/MI355X_MICROARCH.md's hand-off table), not by the HIP memory model,
+// whose own form (release/acquire add, acquire fence: an L2 writeback and invalidate per
+// value block) costs C2 5 %, C1 12 % (profiles/r04/reduce_handoff_mm_ab.txt).  Before the first
+// decomposition of a process whose steps use it, both forms run the same small one-sweep
+// Arnoldi job (two factors, n = 2^18: 1 041 window blocks publishing partials, 24 steps, on a
+// context of its own: no collective, nothing queued on the caller's streams) and must give
+// bitwise the same records; on any difference -- or if the check cannot run -- the process
+// keeps the memory-model form.  TKHIP_RED_MM=0/1 skips the check and forces
+// a form.  tk_reduce_handoff() reports the outcome.
+static std::atomic<int> g_red_state{0};   // 0 not checked, 1 relaxed (checked), 2 MM (mismatch or failure), 3 forced
+static thread_local bool g_in_red_check = false;
+
+static int red_check_run(int device) {
+    const int64_t n = 1 << 18;
+    const int K = 24, nf = 2;
+    std::vector<int64_t> colptr(n + 1), rowval;
+    std::vector<double> nz;
+    rowval.reserve(3 * n);
+    nz.reserve(3 * n);
+    for (int64_t j = 0; j < n; ++j) {   // tridiagonal (-1, 2, -1), column by column
+        colptr[j] = (int64_t)rowval.size();
+        for (int64_t i = j - 1; i <= j + 1; ++i)
+            if (i >= 0 && i < n) {
+                rowval.push_back(i);
+                nz.push_back(i == j ? 2.0 : -1.0);
+            }
+    }
+    colptr[n] = (int64_t)rowval.size();
+    std::vector<double> b0(n), b1(n);
+    for (int64_t i = 0; i < n; ++i) {
+        b0[i] = 1.0 + 0.5 * sin(0.001 * (double)i);
+        b1[i] = 1.0 + 0.25 * cos(0.003 * (double)i) + 1e-3 * (double)(i % 7);
+    }
+    tk_ctx* cc = nullptr;
+    tk_mat* A = nullptr;
+    tk_decomp* dc = nullptr;
+    int verdict = 2;
+    std::vector<double> rec[2];
+    if (tk_ctx_create(device, &cc) == TK_OK &&
+        tk_matrix_from_csc(cc, n, colptr.data(), rowval.data(), nz.data(), 0, &A) == TK_OK) {
+        tk_mat* mats[2] = {A, A};
+        const double* bs[2] = {b0.data(), b1.data()};
+        if (tk_decomp_create(cc, TK_ARNOLDI, nf, 0, nf, mats, bs, n, K, 0, &dc) == TK_OK &&
+            tk_decomp_arnoldi_sweeps(dc) == 1) {
+            bool ok = true;
+            for (int mode = 0; mode < 2 && ok; ++mode) {
+                set_red_mm(mode);
+                rec[mode].assign((size_t)(K + 1) * nf * rec_len(K), 0.0);
+                ok = tk_decomp_init(dc, nullptr) == TK_OK && tk_decomp_sweep(dc, 0, K) == TK_OK &&
+                     tk_decomp_records(dc, 0, K + 1, rec[mode].data()) == TK_OK;
+            }
+            if (ok) verdict = memcmp(rec[0].data(), rec[1].data(), rec[0].size() * sizeof(double)) == 0 ? 1 : 2;
+        }
+    }
+    if (dc) tk_decomp_destroy(dc);
+    if (A) tk_matrix_destroy(A);
+    if (cc) tk_ctx_destroy(cc);
+    return verdict;
+}
+
+static void red_check_once(int device) {
+    if (g_in_red_check) return;
+    int exp = 0;
+    if (!g_red_state.compare_exchange_strong(exp, -1)) {
+        while (g_red_state.load() < 0) std::this_thread::yield();   // (another thread is checking)
+        return;
+    }
+    if (const char* e = getenv("TKHIP_RED_MM")) {
+        set_red_mm(e[0] == '1');
+        g_red_state.store(3);
+        return;
+    }
+    g_in_red_check = true;
+    const int v = red_check_run(device);
+    g_in_red_check = false;
+    set_red_mm(v == 1 ? 0 : 1);
+    if (v != 1)
+        fprintf(stderr, "libtkhip: the relaxed reduce hand-off %s its self-check: using the memory-model form\n",
+                v == 2 ? "failed" : "could not run");
+    g_red_state.store(v);
+}
+
+// 0: the relaxed hand-off (self-checked or forced), 1: the memory-model form, -1: not settled yet
+int tk_reduce_handoff(void) {
+    const int st = g_red_state.load();
+    return st <= 0 ? -1 : red_mm();
+}
+
 tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,
                            tk_mat* const* mats, const double* const* b, int64_t n, int kmax,
                            int track_all_gram, tk_decomp** out) { TK_API_BEGIN
     CHECKARG(c && out && (nf == 0 || (mats && b)), "NULL argument");
+    // (the one-sweep steps' reduce hand-off form, settled once per process)
+    if (method != TK_LANCZOS_REORTH) red_check_once(c->device);
     CHECKARG(method >= TK_ARNOLDI && method <= TK_LANCZOS_REORTH, "unknown method");
     // nf == 0: a rank of a job with more ranks than factors (it only takes part in the
     // records all-reduce; every launch is skipped)

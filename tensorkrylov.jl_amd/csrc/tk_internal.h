@@ -134,6 +134,9 @@ constexpr int ARN_D1_JMAX = 63;
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,
                            unsigned long long seq, hipStream_t s);
 void launch_delay_us(double us, hipStream_t s);   // test-only (TKHIP_TEST_XCH_DELAY_US)
+// k_reduce256's hand-off form (0 relaxed, 1 memory model): process-wide, set before launches
+int red_mm();
+void set_red_mm(int on);
 void launch_fin_vy(const DFac* F, int nf, const KArgs& a, const double* Y, double* X, int ldy, int t, int mode,
                    hipStream_t s);
 void launch_init_a(const DFac* F, int nf, const KArgs& a, hipStream_t s);

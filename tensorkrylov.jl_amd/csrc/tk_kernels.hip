@@ -36,6 +36,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "tk_internal.h"
@@ -1978,6 +1979,10 @@ __global__ __launch_bounds__(1024) void k_red_lan(const DFac* __restrict__ F, KA
 // coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
 // RED_LAN: one-sweep Lanczos step (nv = 6 + j; 6 for factors without a Gram row; the last
 // block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
+// MM: the hand-off in the HIP memory model's own form (release/acquire add + acquire fence);
+// otherwise the measured relaxed form -- chosen per process by red_mm() (tk_abi.cpp's startup
+// self-check compares the two and keeps MM if they ever differ)
+template <bool MM>
 __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
                                                    int coefJ, KArgs ax) {
     __shared__ double rs[16];
@@ -2026,13 +2031,13 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
             // (profiles/r04/reduce_handoff_mm_ab.txt).  ctr's reset below is ordered before the
             // next launch by the kernel boundary.
             __hip_atomic_store(d.RED1 + c, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if TK_RED_MM
-            // memory-model form: the add releases this block's value and acquires the others'
-            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
-#else
-            __builtin_amdgcn_s_waitcnt(0);
-            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
-#endif
+            if constexpr (MM) {
+                // memory-model form: the add releases this block's value and acquires the others'
+                last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
+            } else {
+                __builtin_amdgcn_s_waitcnt(0);
+                last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nv - 1);
+            }
         }
     }
     if (coefJ < 0 && coefJ != RED_LAN) return;
@@ -2041,10 +2046,8 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     const double al_est = coefJ == RED_LAN ? ld(d.sc, SC_ALPHA) : 0.0;
     __syncthreads();
     if (!last) return;
-#if TK_RED_MM
     // (every wave of the last block: its loads ordered after thread 0's acquire)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
+    if constexpr (MM) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     if (coefJ == RED_LAN) {
         lan_step_record(d, ax, (int)blockIdx.y, cld(0), cld(2), cld(3), cld(4), cld(5), al_est,
@@ -3045,15 +3048,25 @@ void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     hipLaunchKernelGGL(k_lan_finalize, dim3(a.npart, nf), dim3(TPB), lds_bytes(a.j + 3, a.kmax, 0), s, F, a);
 }
+// the reduce hand-off form of this process: TK_RED_MM at build time, then tk_abi.cpp's
+// startup self-check (or TKHIP_RED_MM) may switch it to the memory-model form
+static std::atomic<int> g_red_mm{TK_RED_MM};
+int red_mm() { return g_red_mm.load(std::memory_order_relaxed); }
+void set_red_mm(int on) { g_red_mm.store(on ? 1 : 0, std::memory_order_relaxed); }
+
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ,
                    const KArgs* ax) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     KArgs none;
     memset(&none, 0, sizeof(none));
-    if (npart <= 0 && !gate)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
-    else if (npart > 1024 && !gate)   // one partial per tile (k_fin_d)
-        hipLaunchKernelGGL(k_reduce256, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1, none);
+    if (npart <= 0 && !gate) {
+        if (red_mm())
+            hipLaunchKernelGGL(k_reduce256<true>, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
+        else
+            hipLaunchKernelGGL(k_reduce256<false>, dim3(nv, nf), dim3(256), 0, s, F, which, nv, 0, coefJ, ax ? *ax : none);
+    } else if (npart > 1024 && !gate) {   // one partial per tile (k_fin_d)
+        hipLaunchKernelGGL(k_reduce256<false>, dim3(nv, nf), dim3(256), 0, s, F, which, nv, npart, -1, none);
+    }
     else
         hipLaunchKernelGGL(k_reduce, dim3(nv, nf), dim3(64), 0, s, F, which, nv, npart, gate);
 }

@@ -135,3 +135,42 @@ print(json.dumps({"niter": conv.niterations, "orth": list(map(float, conv.orthog
     assert out["1"]["niter"] == out["0"]["niter"] == K
     assert out["1"]["orth"] == out["0"]["orth"]
     assert all(0 < x < 1e-10 for x in out["1"]["orth"][1:]) or method == "TensorLanczos"
+
+
+def test_gram_ahead_converged_within_rounding(ctx):
+    """when the run converges before nmax, the Gram launched behind the last
+    issued step covers more columns than the converged k, and orthogonality_data comes from
+    the leading block of that larger SYRK -- whose k_gram configuration groups the columns
+    differently (a column in the VALU tail at one k sits in an MFMA group at the other), so
+    the sums round differently: equal to TKHIP_GRAM_AHEAD=0 within 1e-13, not bitwise (the
+    non-converging runs above are bitwise).  Laplace d = 3, n = 30 with a smooth RHS at tol
+    1e-2 (converges before nmax = 29, tests/test_gpu_solution.py)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = r'''
+import json, sys
+sys.path[:0] = %r
+import numpy as np
+import tkamd as tk
+ctx = tk.Context(0)
+n, d = 30, 3
+xs = np.arange(1, n + 1) / (n + 1)
+b0 = xs * (1 - xs) + 0.01 * np.random.default_rng(7).random(n)
+b0 = b0 / np.linalg.norm(b0)
+A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
+conv = tk.ConvergenceData(n - 1)
+x = tk.tensorkrylov(conv, A, [b0.copy() for _ in range(d)], 1e-2, n - 1, "TensorArnoldi", ctx=ctx)
+print(json.dumps({"niter": conv.niterations, "conv": x is not None, "orth": list(map(float, conv.orthogonality_data))}))
+''' % (sys.path,)
+    out = {}
+    for v in ("1", "0"):
+        env = dict(os.environ, TKHIP_GRAM_AHEAD=v)
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[v] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["1"]["conv"] and out["0"]["conv"]
+    assert out["1"]["niter"] == out["0"]["niter"] < 29
+    o1, o0 = np.array(out["1"]["orth"][1:]), np.array(out["0"]["orth"][1:])
+    assert np.all(np.isfinite(o1)) and np.abs(o1 - o0).max() <= 1e-13

@@ -24,9 +24,18 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _case(tk, cls):
-    """Golden recorded RHS (experiments/data/reproduction_data, decoded in tests/golden),
-    d = 10, n = 200."""
+def _case(tk, name):
+    """golden10: the recorded RHS of experiments/data/reproduction_data (decoded in
+    tests/golden), d = 10, n = 200, Laplace / ConvDiff -- no convergence within K;
+    smooth3: d = 3, n = 30 Laplace with a smooth RHS, converging at tol 1e-2
+    (tests/test_gpu_solution.py)."""
+    if name == "smooth3":
+        n, d = 30, 3
+        xs = np.arange(1, n + 1) / (n + 1)
+        b0 = xs * (1 - xs) + 0.01 * np.random.default_rng(7).random(n)
+        b0 = b0 / np.linalg.norm(b0)
+        return tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace), [b0.copy() for _ in range(d)]
+    cls = name[len("golden10-"):]
     g = json.load(open(os.path.join(HERE, "golden", "reproduction.json")))
     key = "nonsym_new" if cls == "ConvDiff" else "laplace_new"
     b = np.array(g[key]["rhs"]["10"])
@@ -35,18 +44,19 @@ def _case(tk, cls):
     return kron, [b.copy() for _ in range(10)]
 
 
-@pytest.mark.parametrize("cls,tol,K", [("ConvDiff", 0.1, 60), ("Laplace", 1e-9, 40)])
-def test_emulated_evaluation_split_bitwise(ctx, cls, tol, K):
+@pytest.mark.parametrize("name,tol,K,ranks", [("golden10-ConvDiff", 1e-9, 50, (2, 3, 4)),
+                                             ("golden10-Laplace", 1e-9, 40, (2, 3, 4)),
+                                             ("smooth3", 1e-2, 29, (2, 3))])
+def test_emulated_evaluation_split_bitwise(ctx, name, tol, K, ranks):
     tk = __import__("tkamd")
-    kron, b = _case(tk, cls)
+    kron, b = _case(tk, name)
     d, n = len(b), len(b[0])
     conv1 = tk.ConvergenceData(K)
     x1 = tk.tensorkrylov(conv1, kron, [v.copy() for v in b], tol, K, "TensorArnoldi", ctx=ctx)
     res1 = conv1.native_results
     k_end = conv1.niterations
     assert np.all(res1[1:k_end, 5] >= 0)            # (all evaluated on the single rank)
-    if cls == "ConvDiff":
-        assert x1 is not None                      # this case converges (tol 0.1)
+    assert (x1 is not None) == (name == "smooth3")  # the converging case converges
     # the other factors' records of a full run (bench.py --emulate-ranks)
     A = tk.DeviceMatrix(ctx, kron[0])
     full = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, d, 0, [A] * d, b, K)
@@ -56,7 +66,7 @@ def test_emulated_evaluation_split_bitwise(ctx, cls, tol, K):
     overlay[:K + 1] = full.records(0, K + 1)
     full.close()
     A.close()
-    for N in (2, 3, 4):
+    for N in ranks:
         # (converging: the ranks r != k_end % N end on an iteration another rank evaluated)
         for r in range(N):
             part = tk.Partition(d, N, r, term_split=False)

@@ -24,7 +24,9 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-#define NWIN 4161
+#ifndef NWIN
+#define NWIN 4161   // C2 at one factor (n = 2^20); -DNWIN=525 for C4 (n = 2^17, bandwidth 3)
+#endif
 #define SPIN_MAX (1 << 22)
 typedef double d2 __attribute__((ext_vector_type(2)));
 

@@ -26,7 +26,9 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s line %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-#define NWIN 4161
+#ifndef NWIN
+#define NWIN 4161   // C2 at one factor (n = 2^20); -DNWIN=525 for C4 (n = 2^17, bandwidth 3)
+#endif
 #define SPIN_MAX (1 << 24)
 
 __device__ __forceinline__ void st_sc1(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
