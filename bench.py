@@ -408,6 +408,11 @@ def main():
                 "factor_groups": dev.factor_groups if method == "TensorArnoldi" and sweeps == 1 else 1,
             },
             "host_issue_us_per_iteration": round(host_us_per_step, 2),
+            # the one-sweep reduce hand-off this process runs (tk_reduce_handoff): relaxed
+            # atomics confirmed by the startup self-check, or the memory-model form
+            "reduce_handoff": {0: "relaxed (self-checked against the memory-model form)",
+                               1: "memory-model release/acquire",
+                               2: "relaxed (forced, TKHIP_RED_MM=0)"}.get(L.lib().tk_reduce_handoff(), "unsettled"),
             "end_to_end": e2e,
             "basis_mul_step": {
                 "engine": ("k_fin_vy: flush of the pending column + V*Y from its register row (FP64 FMA), "

@@ -152,7 +152,8 @@ tk_status tk_decomp_agree(tk_decomp* dc, int* vals, int count);
  * (measured correct on gfx950, and confirmed by a self-check against the memory-model form at
  * the process's first tk_decomp_create), 1 = the HIP memory model's release/acquire form (kept
  * when the self-check finds any difference or cannot run; TKHIP_RED_MM=0/1 forces a form),
- * -1 = not settled yet (no decomposition created). */
+ * 2 = relaxed, forced by TKHIP_RED_MM=0 without the check, -1 = not settled yet (no
+ * decomposition created). */
 int tk_reduce_handoff(void);
 
 /* Multi-rank waits (the records exchange, tk_comm_allreduce_host, tk_ctx_sync, destroy) are

@@ -914,10 +914,12 @@ static void red_check_once(int device) {
     g_red_state.store(v);
 }
 
-// 0: the relaxed hand-off (self-checked or forced), 1: the memory-model form, -1: not settled yet
+// 0: the relaxed hand-off, self-checked; 1: the memory-model form; 2: relaxed, forced by
+// TKHIP_RED_MM=0 (no check); -1: not settled yet
 int tk_reduce_handoff(void) {
     const int st = g_red_state.load();
-    return st <= 0 ? -1 : red_mm();
+    if (st <= 0) return -1;
+    return red_mm() ? 1 : (st == 3 ? 2 : 0);
 }
 
 tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,

@@ -231,3 +231,46 @@ def test_exchange_wait_has_a_deadline(monkeypatch):
     A.close()
     c.close()
     assert time.time() - t0 < 30
+
+
+def test_reduce_handoff_self_check(ctx):
+    """the one-sweep reduce's relaxed hand-off is confirmed at the process's
+    first decomposition by a self-check against the memory-model form (tk_reduce_handoff: 0
+    = relaxed, checked; 1 = the check found a difference and the process runs the memory-model
+    form).  Either way the records are bitwise those of the memory-model form: compared here
+    with a process that forces it (TKHIP_RED_MM=1), on a C2-sized factor pair."""
+    import json
+    import subprocess
+    import sys
+    tk = _tk()
+    code = r'''
+import json, sys
+sys.path[:0] = %r
+import numpy as np
+import tkamd as tk
+ctx = tk.Context(0)
+n, K = 1 << 20, 24
+csc = tk.assemble_matrix(n, "Laplace")
+A = tk.DeviceMatrix(ctx, csc)
+bs = [np.random.default_rng(1000 + s).random(n) for s in range(2)]
+dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, 2, 0, [A, A], [b / np.linalg.norm(b) for b in bs], K)
+dev.init(False)
+dev.sweep(0, K)
+r = dev.records(0, K + 1)
+print(json.dumps({"handoff": int(tk._lib.lib().tk_reduce_handoff()), "sweeps": dev.arnoldi_sweeps,
+                  "rec": r.ravel().tolist()}))
+''' % (sys.path,)
+    out = {}
+    for v in (None, "1"):
+        env = dict(os.environ)
+        env.pop("TKHIP_RED_MM", None)
+        if v:
+            env["TKHIP_RED_MM"] = v
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+        assert p.returncode == 0, p.stderr[-2000:]
+        out[v] = json.loads(p.stdout.strip().splitlines()[-1])
+    assert out[None]["sweeps"] == 1
+    assert out[None]["handoff"] in (0, 1)          # settled by the self-check
+    assert out["1"]["handoff"] == 1                 # forced
+    assert out[None]["rec"] == out["1"]["rec"]      # bitwise the memory-model form's records
+    assert tk._lib.lib().tk_reduce_handoff() in (0, 1, 2)
