@@ -144,7 +144,7 @@ def test_gram_ahead_converged_within_rounding(ctx):
     differently (a column in the VALU tail at one k sits in an MFMA group at the other), so
     the sums round differently: equal to TKHIP_GRAM_AHEAD=0 within 1e-13, not bitwise (the
     non-converging runs above are bitwise).  Laplace d = 3, n = 30 with a smooth RHS at tol
-    1e-2 (converges before nmax = 29, tests/test_gpu_solution.py)."""
+    5e-2 (converges near k = 12, well before nmax = 29)."""
     import json
     import os
     import subprocess
@@ -161,7 +161,7 @@ b0 = xs * (1 - xs) + 0.01 * np.random.default_rng(7).random(n)
 b0 = b0 / np.linalg.norm(b0)
 A = tk.KroneckerMatrix.gallery(tk.SymInstance, d, n, tk.Laplace)
 conv = tk.ConvergenceData(n - 1)
-x = tk.tensorkrylov(conv, A, [b0.copy() for _ in range(d)], 1e-2, n - 1, "TensorArnoldi", ctx=ctx)
+x = tk.tensorkrylov(conv, A, [b0.copy() for _ in range(d)], 5e-2, n - 1, "TensorArnoldi", ctx=ctx)
 print(json.dumps({"niter": conv.niterations, "conv": x is not None, "orth": list(map(float, conv.orthogonality_data))}))
 ''' % (sys.path,)
     out = {}

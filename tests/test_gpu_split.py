@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def _case(tk, name):
     """golden10: the recorded RHS of experiments/data/reproduction_data (decoded in
     tests/golden), d = 10, n = 200, Laplace / ConvDiff -- no convergence within K;
-    smooth3: d = 3, n = 30 Laplace with a smooth RHS, converging at tol 1e-2
+    smooth3: d = 3, n = 30 Laplace with a smooth RHS, converging mid-way at tol 5e-2
     (tests/test_gpu_solution.py)."""
     if name == "smooth3":
         n, d = 30, 3
@@ -46,7 +46,7 @@ def _case(tk, name):
 
 @pytest.mark.parametrize("name,tol,K,ranks", [("golden10-ConvDiff", 1e-9, 50, (2, 3, 4)),
                                              ("golden10-Laplace", 1e-9, 40, (2, 3, 4)),
-                                             ("smooth3", 1e-2, 29, (2, 3))])
+                                             ("smooth3", 5e-2, 29, (2, 3))])
 def test_emulated_evaluation_split_bitwise(ctx, name, tol, K, ranks):
     tk = __import__("tkamd")
     kron, b = _case(tk, name)
