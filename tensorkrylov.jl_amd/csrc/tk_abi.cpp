@@ -1492,11 +1492,12 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
 
 // TKHIP_D1_CACHE_MB: the per-step working set (MiB) up to which the one-sweep Arnoldi step
 // loads the basis with the default cache policy instead of nt (0: always nt).  The Infinity
-// Cache is 256 MiB; a line stays resident while everything touched between two uses fits
+// Cache is 256 MiB; a line stays resident while everything touched between two uses fits, and
+// past it the cached loads still paid up to ~450 MB (the A/B in profiles/r05/)
 static double d1_cache_bytes() {
     static const double v = [] {
         const char* e = getenv("TKHIP_D1_CACHE_MB");
-        return (e ? std::max(0.0, atof(e)) : 224.0) * 1048576.0;
+        return (e ? std::max(0.0, atof(e)) : 384.0) * 1048576.0;
     }();
     return v;
 }
@@ -1666,9 +1667,11 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             if (st2) return st2;
         }
         // the basis rows through the caches while this rank's per-step working set (every
-        // local factor's V[:, 0..j) and u in / out, v_j) fits the Infinity Cache: the next step
-        // then re-reads them from there (emulated N = 8, C2: +3..5 %); streamed with nt beyond
-        // (N = 1, C2: -4.5 % with the default policy; profiles/r05/vload_policy_ab.txt)
+        // local factor's V[:, 0..j) and u in / out, v_j) is at most TKHIP_D1_CACHE_MB (384): the
+        // next step then re-reads much of it from the 256 MiB Infinity Cache; streamed with nt
+        // beyond.  Same box, 3 repetitions (profiles/r05/vload_threshold_ab*.txt): C1 +5 %,
+        // emulated C2 N = 8 +4..5 %, C4 +3 %; C2 N = 1 unchanged (its 8 factors pass 384 MB at
+        // j = 3), where the default policy on every step costs 4.5 %
         const bool vcache = (double)nf * 8.0 * (double)dc->ld * (double)(j + 3) <= d1_cache_bytes();
         if (grouped) {
             // each factor group in its own launches on its own stream (the bookkeeping blocks
