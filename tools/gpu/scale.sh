@@ -8,4 +8,4 @@ for N in 2 4 8; do
 done
 for N in 1 2 4 8; do python3 -c "
 import json; d=json.loads(open('gpurun_out/scale_$N.log').read().strip().split('\n')[-1]); e=d.get('end_to_end') or {}
-print("$N", d["value"], d["ms_per_step"], d["roofline"]["achieved"], {k:v["avg_us"] for k,v in d["kernels"].items()}, "e2e", e.get("iterations_s"), e.get("vs_device_steps_only"), "relres==n1", e.get("relres_bitwise_equal_to_n1"), "split", e.get("eval_split"))"; done
+print('$N', d['value'], d['ms_per_step'], d['roofline']['achieved'], {k:v['avg_us'] for k,v in d['kernels'].items()}, 'e2e', e.get('iterations_s'), e.get('vs_device_steps_only'), 'relres==n1', e.get('relres_bitwise_equal_to_n1'), 'split', e.get('eval_split'))"; done
