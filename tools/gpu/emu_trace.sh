@@ -7,6 +7,7 @@ for N in ${@:-8}; do
   tail -1 gpurun_out/emu$N.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('N=$N', d['value'], d['roofline']['avg_launch_us'], {k:v['avg_us'] for k,v in d['kernels'].items()})"
 done
 cd /tmp && export TMPDIR=/tmp
+export TKHIP_RED_MM=0   # (no self-check job in the trace)
 for N in ${@:-8}; do
   rm -rf $R/gpurun_out/emu_tr$N
   timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/emu_tr$N -o run -- python3 $R/bench.py --config ${CFG:-C2} --emulate-rank ${RK:-0} --emulate-ranks $N --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end > $R/gpurun_out/emu_tr$N.log 2>&1 || { echo "trace $N failed"; exit 1; }

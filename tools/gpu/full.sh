@@ -8,6 +8,9 @@ for C in C1 C3 C4; do
   timeout -k 10 300 python bench.py --config $C --steps 4 --warmup 1 --no-cpu-baseline > gpurun_out/bench_$C.log 2>&1 || { echo "bench $C failed"; tail -5 gpurun_out/bench_$C.log; exit 1; }
 done
 cd /tmp && export TMPDIR=/tmp
+# (profiles: the reduce hand-off's startup self-check runs a small one-sweep job of its own,
+# whose kernels would be counted in with the workload's -- relaxed form forced, no check)
+export TKHIP_RED_MM=0
 rm -rf $R/gpurun_out/prof_c2 $R/gpurun_out/pmc_fetch $R/gpurun_out/pmc_write
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_c2 -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-end-to-end > $R/gpurun_out/prof_c2.log 2>&1 || { echo "rocprof failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --pmc-mode > $R/gpurun_out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
