@@ -301,6 +301,11 @@ def main():
                "device_steps_only_iterations_s": round(loop_dev, 2) if loop_dev else None,
                "vs_device_steps_only": round(e2e_rate / loop_dev, 4) if loop_dev else None,
                "eval_split": getattr(conv, "eval_split", None),
+               **({"split_table_eval_us": {"mean": round(float(np.nanmean(eval_overlay[1:, 5])), 1),
+                                           "max": round(float(np.nanmax(eval_overlay[1:, 5])), 1),
+                                           "note": "the full run's per-iteration evaluation times that "
+                                                   "release the other ranks' results in the emulation"}}
+                  if eval_overlay is not None else {}),
                "solves": len(samples),
                "iterations_s_all": [round(max(c_.niterations - 1, 1) / l_, 2) for l_, _, c_ in samples],
                "iterations": int(conv.niterations),
