@@ -745,6 +745,13 @@ struct tk_decomp {
     unsigned long long ahead_want = 0;
     double* Uint = nullptr;
     bool bk_fold = true;    // TKHIP_BK_FOLD=0: every step's bookkeeping as its own k_post
+    // fused one-sweep Arnoldi launches (TKHIP_D1_FUSE): step j's reduce runs in the leading blocks
+    // of step j+1's launch instead of a launch of its own; red_j = the step whose partials are not
+    // reduced yet (-1 none; red_flush launches k_reduce256 for it), wseq = the last step word
+    bool fuse = false;
+    int red_j = -1;
+    unsigned long long wseq = 0;
+    unsigned int* werr = nullptr;           // host-mapped: a fused wait gave up (never, if healthy)
     // exchange signalling without compute-queue markers: k_post blocks add to *xflag, the
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
@@ -815,6 +822,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->gram_scr && !dc->gram_scr_owned_by_allocs) hipFree(dc->gram_scr);
     if (dc->gram_host) hipHostFree(dc->gram_host);
     if (dc->gram_done) hipHostFree(dc->gram_done);
+    if (dc->werr) hipHostFree(dc->werr);
     if (dc->xflag) hipFree(dc->xflag);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
@@ -983,6 +991,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     }
     dc->nvmax = dc->onesweep ? 3 * kmax + 8 : 2 * kmax + 8;
     {
+        // fused one-sweep Arnoldi launches: TKHIP_D1_FUSE=1 on, 0 off; results are bitwise those
+        // of the separate reduce launch (the same reduction, the same coefficients)
+        const char* e = getenv("TKHIP_D1_FUSE");
+        dc->fuse = method == TK_ARNOLDI && dc->onesweep && nf > 0 && e && e[0] == '1';
+    }
+    {
         const char* e = getenv("TKHIP_FIN_D");
         dc->fin_d = !(e && e[0] == '0');
     }
@@ -1059,6 +1073,12 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.lossrow, (size_t)KP * sizeof(double));
         DA(d.ctr, 16);
         DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
+        d.P1b = nullptr;
+        d.rword = nullptr;
+        if (dc->fuse) {
+            DA(d.P1b, (size_t)dc->nvmax * npp * sizeof(double));
+            DA(d.rword, 64);   // (zeroed by dalloc; step words start at 1)
+        }
         const int gi = first_factor + f;
         d.track_gram = (track_all_gram == 1 || method == TK_LANCZOS_REORTH || (gi == 0 && !dc->gram_deferred)) ? 1 : 0;
         dc->any_gram = dc->any_gram || d.track_gram;
@@ -1084,6 +1104,15 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
     }
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+    if (dc->fuse) {
+        void* hp = nullptr;
+        if (hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            free_decomp(dc);
+            return fail(TK_ERR_ALLOC, "tk_decomp_create: fused-launch error word");
+        }
+        dc->werr = (unsigned int*)hp;
+        *dc->werr = 0;
+    }
     // the deferred Gram's partials (tk_decomp_gram), allocated with the rest: an allocation at
     // the first call cost up to ~15 ms inside the driver loop
     if (dc->gram_deferred && nf > 0) {
@@ -1397,6 +1426,10 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.ecol = -1;
     a.mfs = 0;
     a.sl = dc->sl ? 1 : 0;
+    a.red = 0;
+    a.redmm = 0;
+    a.wseq = 0;
+    a.werr = nullptr;
     return a;
 }
 
@@ -1511,8 +1544,27 @@ static void complete_step(tk_decomp* dc, int j, unsigned long long seqj) {
     dc->xs.complete(j + 1);
 }
 
+// Fused one-sweep launches: the reduce of the last step, not yet run in a next launch, as a
+// k_reduce256 of its own (its last block also evaluates the next step's scalars).  Local only.
+static tk_status red_flush(tk_decomp* dc) {
+    if (dc->red_j < 0) return TK_OK;
+    if (dc->werr && __atomic_load_n(dc->werr, __ATOMIC_ACQUIRE))
+        return fail(TK_ERR_INTERNAL, "a fused one-sweep launch's wait for its reducers gave up (TKHIP_D1_FUSE=0 avoids it)");
+    GJOIN(dc);
+    const int j = dc->red_j;
+    dc->red_j = -1;
+    tk_ctx* c = dc->ctx;
+    if (!(dc->skip_mask & 1))
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, (j & 1) ? 5 : 1, 3 * j + 6, 0, c->stream, 0, j + 1), "reduce");
+    return TK_OK;
+}
+
 // The deferred bookkeeping of the last one-sweep step as a k_post of its own.  Local only.
 static tk_status bk_flush(tk_decomp* dc) {
+    {
+        tk_status sr = red_flush(dc);   // (its reduced values first)
+        if (sr) return sr;
+    }
     if (dc->bk_j < 0) return TK_OK;
     GJOIN(dc);
     tk_ctx* c = dc->ctx;
@@ -1565,6 +1617,7 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
         RUN(TCLS_RED, 2, launch_post(dc->df, nf, a, POST_INIT_B, 0, 1, s), "post");
     }
     dc->inited = true;
+    dc->red_j = -1;
     dc->jnext = 0;
     dc->pending = false;
     dc->last_j = -1;
@@ -1673,6 +1726,19 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // emulated C2 N = 8 +4..5 %, C4 +3 %; C2 N = 1 unchanged (its 8 factors pass 384 MB at
         // j = 3), where the default policy on every step costs 4.5 %
         const bool vcache = (double)nf * 8.0 * (double)dc->ld * (double)(j + 3) <= d1_cache_bytes();
+        if (dc->fuse) {
+            // step j-1's reduce in this launch's leading blocks (the pending one: nothing
+            // else has read its values since); otherwise RED1 is complete already
+            a.red = dc->red_j == j - 1 && j > 0 ? 1 : 0;
+            if (dc->red_j >= 0 && !a.red) {
+                tk_status sr = red_flush(dc);
+                if (sr) return sr;
+            }
+            a.redmm = red_mm();
+            a.wseq = a.red ? ++dc->wseq : 0;
+            a.werr = dc->werr;
+            dc->red_j = -1;
+        }
         if (grouped) {
             // each factor group in its own launches on its own stream (the bookkeeping blocks
             // of a group's launch serve that group's factors: host-mirror words offset by g0)
@@ -1685,20 +1751,22 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                 {
                     Timer tm_(c, TCLS_PASS1, 2, sg);
-                    launch_arn_d1(dc->df + g0, ng, a, bg, dc->npd, dc->any_gram, vcache, sg);
+                    launch_arn_d1(dc->df + g0, ng, a, bg, dc->npd, dc->any_gram, vcache, dc->fuse, sg);
                 }
                 LAUNCHCHK("arn_d1");
-                if (!(dc->skip_mask & 1)) {
+                if (!(dc->skip_mask & 1) && !dc->fuse) {
                     Timer tm_(c, TCLS_RED, 2, sg);
                     launch_reduce(dc->df + g0, ng, 1, 3 * j + 6, 0, sg, 0, j + 1);
                 }
                 LAUNCHCHK("reduce");
             }
         } else {
-            RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, vcache, s), "arn_d1");
+            RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, vcache, dc->fuse, s), "arn_d1");
             // (its last block per factor also evaluates the next step's scalars)
-            if (!(dc->skip_mask & 1)) RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
+            if (!(dc->skip_mask & 1) && !dc->fuse)
+                RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
         }
+        if (dc->fuse) dc->red_j = j;   // (reduced in the next launch, or by red_flush)
         dc->bk_j = j;
         dc->bk_args = ax;
         dc->bk_kind = 0;

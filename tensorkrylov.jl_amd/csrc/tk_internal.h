@@ -80,6 +80,10 @@ struct DFac {
     // one-sweep reduce: arrival counter of the step's value blocks (the last one evaluates
     // the next step's scalars, k_reduce256)
     unsigned int* ctr;
+    // fused one-sweep launches (the previous step's reduce in the leading blocks): the odd
+    // steps' partials, and the step word the reducers publish and the window blocks wait for
+    double* P1b;
+    unsigned long long* rword;
 };
 
 struct KArgs {
@@ -105,6 +109,10 @@ struct KArgs {
     int sl;           // 1: V in single-column tiles (column c of a tile at c * 256 doubles, row
                       // stride 8 B) -- the Gram-free one-sweep TensorLanczos, whose step reads one
                       // column and writes one; 0: paired columns (tk_kernels.hip header)
+    int red;          // fused one-sweep launch: its leading blocks reduce step j-1's partials
+    int redmm;        // ... with the memory-model hand-off (red_mm())
+    unsigned long long wseq;   // ... and publish this in each factor's step word (DFac::rword)
+    unsigned int* werr;        // ... a wait that gave up sets this (host-mapped)
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
@@ -147,7 +155,7 @@ void launch_arn_a2(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_arn_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 void launch_init_bd(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, bool vcache,
-                   hipStream_t s);
+                   bool fuse, hipStream_t s);
 void launch_lan_1s(const DFac* F, int nf, const KArgs& a, int npd, hipStream_t s);
 // the gram-free one-sweep Lanczos step (k_lan_1w; npd = the largest DFac::nwl); b.j >= 0: the
 // previous step's record mirror + signal ride in 8 leading blocks

@@ -392,6 +392,49 @@ __device__ __forceinline__ void row_dot2(const Row<MAXC>& R, const double* __res
     sh = a0 + a1;
     sg = b0 + b1;
 }
+// Same, with the coefficients in lanes (lane l holds h[l], g[l]; l < 64 covers MAXC), read
+// column by column with v_readlane into SGPRs: the fused launch's coefficients, produced
+// inside the same launch, come through sc1 vector loads instead of the scalar cache.
+template <int MAXC>
+__device__ __forceinline__ void row_dot2_rl(const Row<MAXC>& R, double hl, double gl, double& sh, double& sg) {
+    static_assert(MAXC <= 64, "one coefficient per lane");
+    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+    const int hlo = __double2loint(hl), hhi = __double2hiint(hl), glo = __double2loint(gl), ghi = __double2hiint(gl);
+#pragma unroll
+    for (int c = 0; c < MAXC; c += 2) {
+        const double h0 = __hiloint2double(__builtin_amdgcn_readlane(hhi, c), __builtin_amdgcn_readlane(hlo, c));
+        const double h1 = __hiloint2double(__builtin_amdgcn_readlane(hhi, c + 1), __builtin_amdgcn_readlane(hlo, c + 1));
+        const double g0 = __hiloint2double(__builtin_amdgcn_readlane(ghi, c), __builtin_amdgcn_readlane(glo, c));
+        const double g1 = __hiloint2double(__builtin_amdgcn_readlane(ghi, c + 1), __builtin_amdgcn_readlane(glo, c + 1));
+        a0 += R.v[c] * h0;
+        a1 += R.v[c + 1] * h1;
+        b0 += R.v[c] * g0;
+        b1 += R.v[c + 1] * g1;
+    }
+    sh = a0 + a1;
+    sg = b0 + b1;
+}
+// an agent-scope (sc1) load: another CU's in-launch store drained to the device level is seen
+__device__ __forceinline__ double ld_ag(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Fused one-sweep launch: one lane polls the factor's step word (sc1 loads, s_sleep between)
+// until the in-launch reducers publish `want`; the block's waves pass a barrier after it.
+// Bounded: after ~2^22 polls the error word is set (the host reports TK_ERR_INTERNAL) and the
+// block goes on -- a result would be wrong, but nothing hangs.
+__device__ __forceinline__ void fuse_wait(const unsigned long long* word, unsigned long long want, unsigned int* err) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+            if (++spins > (1u << 22)) {
+                if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
 // Same, with columns c < LC read from LDS (pair p of this thread's row at vl[p * TPB + t], zero
 // for rows outside the basis) as each chunk of 8 is reached: the same order, so bitwise equal.
 template <int MAXC, int LC>
@@ -995,8 +1038,11 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #define D1_PHASE(k) do { } while (0)
 #endif
 __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds);
+template <bool MM, bool FUSED>
+__device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int which, int nv, int np, int coefJ,
+                                             const KArgs& ax, unsigned long long wseq);
 __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent = false);
-template <int MAXC, int FMT, bool VC>
+template <int MAXC, int FMT, int MODE>
 #ifndef TK_D1_OCCT
 #define TK_D1_OCCT 2
 #endif
@@ -1017,6 +1063,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                                                                                                   KArgs b) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
     constexpr int LC = D1_LCOLS(MAXC);   // low columns of the row kept in LDS (TK_D1_LC)
+    // MODE bit 0 (VC): the basis rows through the caches (the launcher's choice while the rank's
+    // per-step working set fits the Infinity Cache), else nt.  Bit 1 (FUSE): the previous step's
+    // reduce runs in this launch's leading blocks (a.red) -- the window blocks issue their row
+    // loads, wait for the factor's step word, and read the coefficients the reducers produced in
+    // this launch through sc1 vector loads; partials alternate between P1 / P1b by step parity
+    constexpr bool VC = MODE & 1, FUSE = (MODE & 2) != 0;
+    static_assert(!FUSE || LC == 0, "fused launches keep the whole register row in VGPRs");
     static_assert(LC % 8 == 0 && (LC == 0 || LC <= MAXC - 8), "LDS columns: whole chunks of 8, below the patched pairs");
     __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
 #if TK_D1_COEF_LDS
@@ -1034,11 +1087,26 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // factors x, x+8, .. -- dispatched first, they finish while the windows stream (as
     // trailing blocks they lengthened short launches by their own duration) -- and the window
     // blocks do not wait for them.
-    const int x0 = b.j >= 0 ? 8 : 0;
+    // fused: XR leading reducer blocks (row 0; value c of factor f at x = f * NVR + c), then the
+    // bookkeeping blocks, then the windows -- every block a window waits for is dispatched first
+    const int NVR = (FUSE && a.red) ? 3 * a.j + 3 : 0;
+    const int XR = (FUSE && a.red) ? (((int)gridDim.y * NVR + 7) & ~7) : 0;
+    if (FUSE && (int)blockIdx.x < XR) {
+        const int f = (int)blockIdx.x / NVR, c = (int)blockIdx.x - f * NVR;
+        if (blockIdx.y == 0 && f < (int)gridDim.y) {
+            // step j-1's reduce (k_reduce256's block; its last block evaluates this step's scalars)
+            const int jp = a.j - 1;
+            if (a.redmm) red256_block<true, true>(F[f], f, c, (jp & 1) ? 5 : 1, 3 * jp + 6, 0, jp + 1, a, a.wseq);
+            else red256_block<false, true>(F[f], f, c, (jp & 1) ? 5 : 1, 3 * jp + 6, 0, jp + 1, a, a.wseq);
+        }
+        return;
+    }
+    const int x0 = XR + (b.j >= 0 ? 8 : 0);
     if ((int)blockIdx.x < x0) {
         if (blockIdx.y == 0 && !(TK_BK_TEST & 2))   // (TK_BK_TEST: timing experiments)
-            for (int f = blockIdx.x; f < (int)gridDim.y; f += 8) {
+            for (int f = (int)blockIdx.x - XR; f < (int)gridDim.y; f += 8) {
                 const DFac& df = F[f];
+                if (FUSE && a.red) fuse_wait(df.rword, a.wseq, a.werr);
                 bk_arn_d(df, b, b.rec + (int64_t)df.gidx * b.m, lds);
                 if (!(TK_BK_TEST & 1)) post_signal(b, df, f, true, true);
                 __syncthreads();
@@ -1125,8 +1193,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // the step's scalars, evaluated by the last block of the previous step's reduce
         // (k_reduce256): RED1 = [c (j) | q (j) | |u|^2, <u,z>, .. (3j+3 values) | ib, gamma, ..]
         const double* s1 = d.RED1 + (j > 0 ? 3 * j + 3 : 2);
-        const double inv_beta = CP4(s1)[D1S_IB], gamma = CP4(s1)[D1S_GAMMA];
+        double inv_beta, gamma;
         double sc, sq;
+        if constexpr (FUSE) {
+            // (the row loads above are in flight while the reducers of this launch finish)
+            if (a.red) fuse_wait(d.rword, a.wseq, a.werr);
+            inv_beta = ld_ag(s1 + D1S_IB);
+            gamma = ld_ag(s1 + D1S_GAMMA);
+            // lane l holds c[l] and q[l]; row_dot2_rl broadcasts them column by column (the same
+            // values and FMA order as the scalar-cache form: bitwise the same sums)
+            const int l = t & 63;
+            row_dot2_rl<MAXC>(R, ld_ag(d.RED1 + l), ld_ag(d.RED1 + j + l), sc, sq);
+        } else {
+            inv_beta = CP4(s1)[D1S_IB];
+            gamma = CP4(s1)[D1S_GAMMA];
 #if TK_D1_COEF_LDS
         row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sq);
 #else
@@ -1137,6 +1217,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             row_dot2<MAXC>(R, c, qv, sc, sq);
         }
 #endif
+        }
         D1_PHASE(0);
         // v_j = (u_j - V c) ib.  With h1 = V'A v_j = (q - Hbar c) ib (CGS's first projection;
         // q = V'A u_j from the previous sweep) and A v_j = (A u_j - A V c) ib, the Arnoldi
@@ -1287,7 +1368,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
             if (col < j) vi = 2 * j + 6 + col;
         }
-        if (vi >= 0) st_wt(d.P1, (int64_t)vi * d.npd + slot, sum);
+        if (vi >= 0) st_wt((FUSE && (j & 1)) ? d.P1b : d.P1, (int64_t)vi * d.npd + slot, sum);
     }
 #if TK_D1_TRACE
     __syncthreads();
@@ -1982,19 +2063,23 @@ __global__ __launch_bounds__(1024) void k_red_lan(const DFac* __restrict__ F, KA
 // MM: the hand-off in the HIP memory model's own form (release/acquire add + acquire fence);
 // otherwise the measured relaxed form -- chosen per process by red_mm() (tk_abi.cpp's startup
 // self-check compares the two and keeps MM if they ever differ)
-template <bool MM>
-__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
-                                                   int coefJ, KArgs ax) {
+// FUSED (a fused one-sweep launch's leading blocks, k_arn_d1 with a pending reduce): the last
+// block stores the scalars with agent-scope atomics, waits for them, then publishes `wseq` in the
+// factor's step word -- the in-launch hand-off row of /opt/skills/guides/MI355X_MICROARCH.md
+// (every store of the handed-off bytes sc1 and drained before the flag, every load of them sc1).
+// which: 1 P1 -> RED1, 2 P2 -> RED2, 3 P1 -> RED2, 5 P1b -> RED1 (the odd steps' partials of a
+// fused handle).
+template <bool MM, bool FUSED>
+__device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int which, int nv, int np, int coefJ,
+                                             const KArgs& ax, unsigned long long wseq) {
     __shared__ double rs[16];
     __shared__ int last;
-    const DFac& d = F[blockIdx.y];
-    const int c = blockIdx.x;
     const int nvs = nv;   // (the scalars' place after the values)
     if (coefJ == RED_LAN && !d.track_gram) nv = 6;
     if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
     const int npart = np > 0 ? np : d.npd;
-    const double* P = (which == 2 ? d.P2 : d.P1) + (int64_t)c * npart;   // which 3: P1 -> RED2
+    const double* P = (which == 2 ? d.P2 : (which == 5 ? d.P1b : d.P1)) + (int64_t)c * npart;   // which 3: P1 -> RED2
     const int t = threadIdx.x;
     double s = 0.0;
     for (int b0 = 0; b0 < npart; b0 += 6144) {   // one round up to 6144 partials (n ~ 1.5M)
@@ -2050,7 +2135,7 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
     if constexpr (MM) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     auto cld = [&](int i) { return __hip_atomic_load(d.RED1 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
     if (coefJ == RED_LAN) {
-        lan_step_record(d, ax, (int)blockIdx.y, cld(0), cld(2), cld(3), cld(4), cld(5), al_est,
+        lan_step_record(d, ax, fidx, cld(0), cld(2), cld(3), cld(4), cld(5), al_est,
                         [&](int c) { return cld(6 + c); });
         return;
     }
@@ -2077,12 +2162,28 @@ __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, i
         const double ib = 1.0 / beta;
         const double t1 = (uz - cq) * ib;
         double* o = d.RED1 + nvs;
-        st(o, D1S_IB, ib);
-        st(o, D1S_GAMMA, t1 * ib);
-        st(o, D1S_BETA, beta);
-        st(o, D1S_T1, t1);
+        if constexpr (FUSED) {
+            st_wt(o, D1S_IB, ib);
+            st_wt(o, D1S_GAMMA, t1 * ib);
+            st_wt(o, D1S_BETA, beta);
+            st_wt(o, D1S_T1, t1);
+        } else {
+            st(o, D1S_IB, ib);
+            st(o, D1S_GAMMA, t1 * ib);
+            st(o, D1S_BETA, beta);
+            st(o, D1S_T1, t1);
+        }
         __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (FUSED) {
+            __builtin_amdgcn_s_waitcnt(0);   // (the scalars and the values are through to the device)
+            __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
+}
+template <bool MM>
+__global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
+                                                   int coefJ, KArgs ax) {
+    red256_block<MM, false>(F[blockIdx.y], (int)blockIdx.y, (int)blockIdx.x, which, nv, np, coefJ, ax, 0ull);
 }
 
 // ------------------------------------------------------------------ post-processing
@@ -2219,10 +2320,11 @@ __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds
         for (int q = 0; q < 8; ++q)
             if (e0 + q * TPB + t < HN) Hs[e0 + q * TPB + t] = hv[q];
     }
-    for (int i = t; i < nv; i += TPB) red[i] = ld(d.RED1, i);
+    // (RED1 through sc1 loads: in a fused launch the reducers of the same launch wrote it)
+    for (int i = t; i < nv; i += TPB) red[i] = ld_ag(d.RED1 + i);
     for (int i = t; i <= j; i += TPB) Hs[j * J2 + i] = ld(d.g, i);
     const double bnorm = ld(d.sc, SC_BNORM);
-    const double beta = ld(d.RED1, nv + D1S_BETA), ib = ld(d.RED1, nv + D1S_IB), t1 = ld(d.RED1, nv + D1S_T1);
+    const double beta = ld_ag(d.RED1 + nv + D1S_BETA), ib = ld_ag(d.RED1 + nv + D1S_IB), t1 = ld_ag(d.RED1 + nv + D1S_T1);
     __syncthreads();
     for (int i = t; i <= j; i += TPB) {
         const double ci = red[i];
@@ -2970,7 +3072,7 @@ void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     });
 }
 void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, bool vcache,
-                   hipStream_t s) {
+                   bool fuse, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
@@ -2978,15 +3080,19 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     // [ LDS columns (TK_D1_LC) | column-dot slots: (u,z) chunks + scalars (+ Gram chunks) ]
     size_t lds = ((size_t)D1_LCOLS(M) * TPB + (size_t)(M / 8 + 1 + (gram ? (M + 15) / 16 : 0)) * D1_CHW) * sizeof(double);
     if (b.j >= 0) lds = std::max(lds, bk_lds_doubles(b.j) * sizeof(double));
-    const int gx = TK_D1_ONEWIN ? (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
+    // (fused with a pending reduce: nf * (3j + 3) leading reducer blocks, rounded to whole XCD rounds)
+    const int xr = (fuse && a.red) ? (nf * (3 * a.j + 3) + 7) & ~7 : 0;
+    const int gx = TK_D1_ONEWIN ? xr + (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
     with_band_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
-            if (vcache)
-                hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value, true>), dim3(gx, nf), dim3(TPB),
-                                   lds, s, F, a, b);
-            else
-                hipLaunchKernelGGL((k_arn_d1<decltype(M)::value, decltype(FM)::value, false>), dim3(gx, nf), dim3(TPB),
-                                   lds, s, F, a, b);
+            constexpr int MV = decltype(M)::value, FV = decltype(FM)::value;
+            if (fuse) {
+                if (vcache) hipLaunchKernelGGL((k_arn_d1<MV, FV, 3>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+                else hipLaunchKernelGGL((k_arn_d1<MV, FV, 2>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+            } else {
+                if (vcache) hipLaunchKernelGGL((k_arn_d1<MV, FV, 1>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+                else hipLaunchKernelGGL((k_arn_d1<MV, FV, 0>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+            }
         });
     });
 }
