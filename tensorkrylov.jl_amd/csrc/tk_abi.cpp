@@ -756,6 +756,14 @@ struct tk_decomp {
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
     unsigned long long xcount = 0;
+    // factor groups under an exchange: one signal word per local factor (DFac::xsig, its value
+    // at create in xsig0); a slot is complete when every factor's word shows xscnt[slot] steps
+    std::vector<unsigned long long*> xsig;
+    std::vector<unsigned long long> xsig0, xscnt;
+    unsigned long long xstep = 0;
+    // TKHIP_TEST_GROUP_DELAY_US (tests, read at create): group 0's stream held back this long
+    // before each grouped launch, so the other groups run steps ahead of it
+    double gdelay_us = 0.0;
     // single rank: records also land in host-mapped memory with a per-factor sequence word,
     // so tk_decomp_records waits for exactly its steps (not for the whole queue)
     double* hrec = nullptr;                 // [(kmax+2) slots][d_total][m]
@@ -824,6 +832,7 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->gram_done) hipHostFree(dc->gram_done);
     if (dc->werr) hipHostFree(dc->werr);
     if (dc->xflag) hipFree(dc->xflag);
+    for (unsigned long long* p : dc->xsig) hipFree(p);
     if (dc->stallw) hipFree(dc->stallw);
     if (dc->hrec) hipHostFree(dc->hrec);
     if (dc->hdone) hipHostFree(dc->hdone);
@@ -1140,6 +1149,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
     if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
+    if (const char* eg = getenv("TKHIP_TEST_GROUP_DELAY_US")) dc->gdelay_us = std::max(0.0, atof(eg));
     if (const char* ek = getenv("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
     if (const char* eb = getenv("TKHIP_BK_FOLD")) dc->bk_fold = eb[0] != '0';
     dc->bk_fold = dc->bk_fold && TK_D1_ONEWIN;   // (the window-loop kernel has no bookkeeping blocks)
@@ -1204,6 +1214,35 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
                   hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
         for (int g = 0; ok && g < G - 1; ++g)
             ok = hipEventCreateWithFlags(&dc->fev_join[g], hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
+        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");   // (diagnostics: the round-4 shared word)
+        if (ok && dc->recv != dc->rec && !(esh && esh[0] == '1')) {
+            // the groups' streams run apart (one may be a step ahead of another), so a shared
+            // count can be reached with a step of one group missing: each factor signals its
+            // own word and the exchange waits for every word (exchange_range)
+            for (int f = 0; ok && f < nf; ++f) {
+                void* p = nullptr;
+                unsigned long long v0 = 0;
+                ok = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p;
+                if (ok) {
+                    dc->xsig.push_back((unsigned long long*)p);
+                    ok = hipMemcpy(&v0, p, 8, hipMemcpyDeviceToHost) == hipSuccess;
+                }
+                dc->xsig0.push_back(v0);
+            }
+            for (int f = 0; ok && f < nf; ++f) dc->hf[f].xsig = dc->xsig[f];
+            ok = ok && hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) == hipSuccess;
+            if (!ok) {   // (no groups then: the one shared word)
+                for (unsigned long long* p : dc->xsig) hipFree(p);
+                dc->xsig.clear();
+                dc->xsig0.clear();
+                for (int f = 0; f < nf; ++f) dc->hf[f].xsig = nullptr;
+                if (hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) != hipSuccess) {
+                    free_decomp(dc);
+                    return fail(TK_ERR_HIP, "upload descriptors");
+                }
+            }
+            dc->xscnt.assign(kmax + 2, 0);
+        }
         if (ok) {
             dc->ngr = G;
             for (int g = 0; g <= G; ++g) dc->gst[g] = g * nf / G;
@@ -1448,8 +1487,14 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
     // start when the steps' k_post blocks have signalled (the count at which slot s1 was
     // written); init / flush slots and handles without the signal word after an event marker
     if (dc->xflag && s0 >= 1 && s1 <= dc->kmax) {
-        HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcnt[s1], hipStreamWaitValueGte,
-                                    0xFFFFFFFFFFFFFFFFull));
+        if (!dc->xsig.empty()) {   // (factor groups: every factor's own count)
+            for (size_t f = 0; f < dc->xsig.size(); ++f)
+                HIPCHK(hipStreamWaitValue64(c->xstream, dc->xsig[f], dc->xsig0[f] + dc->xscnt[s1],
+                                            hipStreamWaitValueGte, 0xFFFFFFFFFFFFFFFFull));
+        } else {
+            HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcnt[s1], hipStreamWaitValueGte,
+                                        0xFFFFFFFFFFFFFFFFull));
+        }
     } else {
         HIPCHK(hipEventRecord(dc->ev_c[s1], c->stream));
         HIPCHK(hipStreamWaitEvent(c->xstream, dc->ev_c[s1], 0));
@@ -1541,6 +1586,7 @@ static void complete_step(tk_decomp* dc, int j, unsigned long long seqj) {
     if (dc->xflag) dc->xcount += (unsigned long long)dc->nf;   // one add per factor
     if (dc->hdone) dc->slot_seq[j + 1] = seqj;
     dc->xcnt[j + 1] = dc->xcount;
+    if (!dc->xsig.empty()) dc->xscnt[j + 1] = ++dc->xstep;
     dc->xs.complete(j + 1);
 }
 
@@ -1625,6 +1671,7 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     // a new sequence: slots of the previous one that never went out are dropped (on every rank)
     dc->xs.reset();
     dc->xcnt[0] = dc->xcount;
+    if (!dc->xsig.empty()) dc->xscnt[0] = dc->xstep;
     dc->xs.complete(0);
     if (dc->recv != dc->rec) {
         st = xsend(dc, dc->xs.need(0));
@@ -1747,6 +1794,10 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             for (int g = 0; g < dc->ngr; ++g) {
                 const int g0 = dc->gst[g], ng = dc->gst[g + 1] - dc->gst[g];
                 hipStream_t sg = grp_stream(dc, g);
+                if (g == 0 && dc->gdelay_us > 0) {   // (tests: the other groups run ahead)
+                    launch_delay_us(dc->gdelay_us, sg);
+                    LAUNCHCHK("group delay");
+                }
                 KArgs bg = b;
                 if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                 {

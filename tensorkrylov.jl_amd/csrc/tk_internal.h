@@ -84,6 +84,10 @@ struct DFac {
     // steps' partials, and the step word the reducers publish and the window blocks wait for
     double* P1b;
     unsigned long long* rword;
+    // factor groups under a records exchange: this factor's own exchange signal word (the
+    // groups' streams run apart, so one shared count could be reached with a step of one group
+    // missing and another group's next step counted instead); null: KArgs::xflag
+    unsigned long long* xsig;
 };
 
 struct KArgs {

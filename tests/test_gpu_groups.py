@@ -110,6 +110,46 @@ def test_factor_groups_under_records_exchange(ctx, grp, monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_factor_groups_exchange_waits_for_every_group(ctx, fuse, monkeypatch):
+    """The groups' streams run apart: with group 0's stream held back before every launch
+    (TKHIP_TEST_GROUP_DELAY_US) group 1 runs steps ahead, and a shared signal count could then
+    be reached with group 0's row of a slot still unwritten (the exchanged record read as
+    zeros -- seen once with the fused launches).  Each factor signals its own word and the
+    exchange waits for all of them: the exchanged records equal the one-stream local run bit for
+    bit, with and without the fused launches."""
+    import tkamd as tk
+    d, n, K = 3, 1 << 15, 30
+    monkeypatch.setenv("TKHIP_D1_FUSE", fuse)
+    rng = np.random.default_rng(12)
+    mat = tk.assemble_matrix(n, "ConvDiff")
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+
+    def run(c, G):
+        monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
+        A = tk.DeviceMatrix(c, mat)
+        dev = tk.DeviceDecomposition(c, 0, d, 0, [A] * d, bs, K)
+        assert dev.factor_groups == int(G)
+        dev.init(False)
+        dev.sweep(0, K)
+        r = dev.records(0, K + 1)
+        dev.close()
+        A.close()
+        return r
+
+    local = run(ctx, "1")
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_TEST_GROUP_DELAY_US", "300")
+    try:
+        for _ in range(2):
+            assert np.array_equal(local, run(c2, "2"))
+    finally:
+        monkeypatch.delenv("TKHIP_TEST_GROUP_DELAY_US")
+        c2.close()
+
+
 @pytest.mark.parametrize("d", [2, 5])
 def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
     """One-sweep TensorLanczos without Gram rows (k_lan_1w + k_red_lan, the deferred Gram)
