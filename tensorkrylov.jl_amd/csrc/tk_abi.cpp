@@ -1001,9 +1001,27 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     dc->nvmax = dc->onesweep ? 3 * kmax + 8 : 2 * kmax + 8;
     {
         // fused one-sweep Arnoldi launches: TKHIP_D1_FUSE=1 on, 0 off; results are bitwise those
-        // of the separate reduce launch (the same reduction, the same coefficients)
+        // of the separate reduce launch (the same reduction, the same coefficients).  Unset: on
+        // when the local factors step as factor groups (two streams) over at most
+        // TKHIP_D1_FUSE_WINDOWS (2048) windows in all -- C4 at N = 8 / 4 (2 / 3 factors of 525
+        // windows: +6..16 % / +3 %); off for one factor (C4 rank 7 -1..3 %, C2 N = 8 -7 %) and for
+        // larger grids (C4 N = 1's 5250 windows -9 %, C2 N = 2 / 4 -8..11 %), where the window
+        // blocks waiting for the reducers cost more than the launch they save
+        // (profiles/r05/fused_launch_ab*.txt)
         const char* e = getenv("TKHIP_D1_FUSE");
-        dc->fuse = method == TK_ARNOLDI && dc->onesweep && nf > 0 && e && e[0] == '1';
+        bool want = e ? e[0] == '1' : false;
+        if (!e) {
+            const char* eg = getenv("TKHIP_FACTOR_GROUPS");
+            const char* ew = getenv("TKHIP_D1_FUSE_WINDOWS");
+            const long wmax = ew ? atol(ew) : 2048;
+            long wins = 0;
+            for (int f = 0; f < nf; ++f) {
+                const int ws = 256 - 2 * (mats[f]->hl + mats[f]->hu);
+                wins += ws > 0 ? (long)((n + ws - 1) / ws) : 0;
+            }
+            want = nf >= 2 && !(eg && atoi(eg) <= 1) && wins <= wmax;
+        }
+        dc->fuse = method == TK_ARNOLDI && dc->onesweep && nf > 0 && want;
     }
     {
         const char* e = getenv("TKHIP_FIN_D");
