@@ -870,10 +870,13 @@ tk_status tk_solver_run(tk_solver* sv, tk_decomp* dc, double tol, int kfirst, in
             pool.done[w] = 0;
         }
         inflight[w] = k;
-        if (hp && k >= klast - hot_iters()) hp->set_hot(true);
+        // (split: the tail is this rank's last owned iterations, one in NR of the last ones --
+        // e.g. C4 at N = 8, rank 7's k = 47 took 127 us on one thread, the loop's end waiting
+        // for it; profiles/r05/e2e_trace_split_tail.txt)
+        if (hp && k >= klast - hot_iters() * NR) hp->set_hot(true);
         {
             std::lock_guard<std::mutex> lk(workers[w]->mu);
-            workers[w]->ws.nthreads = k > klast - tail_iters() ? tail : 1;
+            workers[w]->ws.nthreads = k > klast - tail_iters() * NR ? tail : 1;
             workers[w]->ws.par = hp;
             workers[w]->job = k;
         }
