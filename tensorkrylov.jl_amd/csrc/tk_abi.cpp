@@ -37,6 +37,45 @@
 
 using namespace tk;
 
+// ------------------------------------------------------------------ host issue profile
+// TKHIP_HOST_PROFILE=1 (diagnostics): host time spent in each part of a step's issue, summed
+// over the process and printed to stderr at exit -- where the 8-15 us per step of
+// tk_decomp_step go (launches, exchange calls, event queries, the rest)
+enum { HP_STEP = 0, HP_D1, HP_RED, HP_GUARD, HP_XCH, HP_NCCL, HP_MIRROR, HP_BK, HP_N };
+static const char* const hp_name[HP_N] = {"tk_decomp_step (all)", "k_arn_d1 launch", "k_reduce256 launch",
+                                          "slot guard", "exchange_range (all)", "ncclAllReduce",
+                                          "mirror launch", "bk/complete/xsched"};
+struct HostProf {
+    bool on = false;
+    double us[HP_N] = {};
+    long n[HP_N] = {};
+    HostProf() {
+        const char* e = getenv("TKHIP_HOST_PROFILE");
+        on = e && e[0] == '1';
+    }
+    ~HostProf() {
+        if (!on || !n[HP_STEP]) return;
+        fprintf(stderr, "[tkhip host profile] %ld steps\n", n[HP_STEP]);
+        for (int i = 0; i < HP_N; ++i)
+            if (n[i])
+                fprintf(stderr, "  %-24s %8ld calls %9.2f us/call %7.2f us/step\n", hp_name[i], n[i], us[i] / n[i],
+                        us[i] / n[HP_STEP]);
+    }
+};
+static HostProf g_hp;
+struct HpScope {
+    int i;
+    std::chrono::steady_clock::time_point t0;
+    explicit HpScope(int i_) : i(g_hp.on ? i_ : -1) {
+        if (i >= 0) t0 = std::chrono::steady_clock::now();
+    }
+    ~HpScope() {
+        if (i < 0) return;
+        g_hp.us[i] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        ++g_hp.n[i];
+    }
+};
+
 // ------------------------------------------------------------------ errors
 // a fixed buffer: recording an error never allocates (a bad_alloc is itself reported here)
 static thread_local char g_err[1024];
@@ -1428,6 +1467,7 @@ static hipStream_t grp_stream(tk_decomp* dc, int g) {
 // Before a slot's send rows are rewritten, the previous all-reduce of that slot must
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
+    HpScope hp_(HP_GUARD);
     // (an already completed exchange needs no wait packet in the compute queue)
     if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess) {
         HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
@@ -1495,6 +1535,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
 // factor's record.  Slots [s0, s1] are contiguous in memory, so a range is one call.
 // Which ranges go out when is decided by dc->xs (tk_xsched.h), identically on every rank.
 static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
+    HpScope hp_(HP_XCH);
     tk_ctx* c = dc->ctx;
     STUCKCHK(c);
     const size_t cnt = (size_t)dc->d_total * dc->m;
@@ -1533,6 +1574,7 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
             launch_delay_us(delay_us, c->xstream);
             LAUNCHCHK("xch delay");
         }
+        HpScope hp_n(HP_NCCL);
         NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
     }
     HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));
@@ -1540,6 +1582,7 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
     if (dc->xdone) {
         ++dc->seq;
         for (int sl = s0; sl <= s1; ++sl) dc->xslot_seq[sl] = dc->seq;
+        HpScope hp_m(HP_MIRROR);
         launch_mirror_records(r, dc->hrec + (size_t)s0 * cnt, (int)tot, dc->xdone + s0, s1 - s0 + 1, dc->seq,
                               c->xstream);
         LAUNCHCHK("mirror_records");
@@ -1820,20 +1863,27 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 if (bg.j >= 0 && bg.hdone) bg.hdone += g0;
                 {
                     Timer tm_(c, TCLS_PASS1, 2, sg);
+                    HpScope hp_(HP_D1);
                     launch_arn_d1(dc->df + g0, ng, a, bg, dc->npd, dc->any_gram, vcache, dc->fuse, sg);
                 }
                 LAUNCHCHK("arn_d1");
                 if (!(dc->skip_mask & 1) && !dc->fuse) {
                     Timer tm_(c, TCLS_RED, 2, sg);
+                    HpScope hp_(HP_RED);
                     launch_reduce(dc->df + g0, ng, 1, 3 * j + 6, 0, sg, 0, j + 1);
                 }
                 LAUNCHCHK("reduce");
             }
         } else {
-            RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, vcache, dc->fuse, s), "arn_d1");
+            {
+                HpScope hp_(HP_D1);
+                RUN(TCLS_PASS1, 2, launch_arn_d1(dc->df, nf, a, b, dc->npd, dc->any_gram, vcache, dc->fuse, s), "arn_d1");
+            }
             // (its last block per factor also evaluates the next step's scalars)
-            if (!(dc->skip_mask & 1) && !dc->fuse)
+            if (!(dc->skip_mask & 1) && !dc->fuse) {
+                HpScope hp_(HP_RED);
                 RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
+            }
         }
         if (dc->fuse) dc->red_j = j;   // (reduced in the next launch, or by red_flush)
         dc->bk_j = j;
@@ -1976,6 +2026,7 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     if (j != dc->jnext) return fail(TK_ERR_STATE, "step %d requested, next step is %d", j, dc->jnext);
     if (j >= dc->kmax) return fail(TK_ERR_ARG, "step %d >= kmax %d", j, dc->kmax);
     HIPCHK(hipSetDevice(dc->ctx->device));
+    HpScope hp_step(HP_STEP);
     const int prev_bk = dc->bk_j;
     const unsigned long long prev_seq = dc->bk_args.seq;
     tk_status st = j == dc->fail_step ? fail(TK_ERR_HIP, "step %d: injected failure (TKHIP_TEST_FAIL_STEP)", j)
@@ -1986,6 +2037,7 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
         dc->failed = true;
         return st;
     }
+    HpScope hp_bk(HP_BK);
     if (dc->bk_j == j) {
         // one sweep: this launch carried step j-1's bookkeeping (its record is complete);
         // step j's own waits for the next launch unless the caller wants it now
