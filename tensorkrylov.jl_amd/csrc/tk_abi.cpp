@@ -41,10 +41,10 @@ using namespace tk;
 // TKHIP_HOST_PROFILE=1 (diagnostics): host time spent in each part of a step's issue, summed
 // over the process and printed to stderr at exit -- where the 8-15 us per step of
 // tk_decomp_step go (launches, exchange calls, event queries, the rest)
-enum { HP_STEP = 0, HP_D1, HP_RED, HP_GUARD, HP_XCH, HP_NCCL, HP_MIRROR, HP_BK, HP_N };
+enum { HP_STEP = 0, HP_D1, HP_RED, HP_GUARD, HP_XCH, HP_NCCL, HP_MIRROR, HP_BK, HP_GQ, HP_N };
 static const char* const hp_name[HP_N] = {"tk_decomp_step (all)", "k_arn_d1 launch", "k_reduce256 launch",
                                           "slot guard", "exchange_range (all)", "ncclAllReduce",
-                                          "mirror launch", "bk/complete/xsched"};
+                                          "mirror launch", "bk/complete/xsched", "slot guard: event query"};
 struct HostProf {
     bool on = false;
     double us[HP_N] = {};
@@ -1468,8 +1468,23 @@ static hipStream_t grp_stream(tk_decomp* dc, int g) {
 // have finished reading them.
 static tk_status slot_guard(tk_decomp* dc, int slot) {
     HpScope hp_(HP_GUARD);
-    // (an already completed exchange needs no wait packet in the compute queue)
-    if (dc->recv != dc->rec && hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess) {
+    if (dc->recv == dc->rec) return TK_OK;
+    // The host-mapped mirror word answers first: an exchange is mirrored (xdone) on the
+    // exchange stream right after its all-reduce, so a slot never exchanged (xslot_seq 0) or
+    // whose last exchange is mirrored has no reader of its send rows left -- one host load.
+    // Not mirrored yet (the host issuing ahead of the device: the bench's back-to-back sweeps,
+    // the solver's steps ahead) the wait packet goes in directly; hipEventQuery cost 2-5 us of
+    // host time per step there, the most of any call after the launches (TKHIP_HOST_PROFILE)
+    bool need = true;
+    if (dc->xdone) {
+        const unsigned long long want = dc->xslot_seq[slot];
+        if (want == 0 || __atomic_load_n(dc->xdone + slot, __ATOMIC_ACQUIRE) >= want) return TK_OK;
+    } else {
+        // (an already completed exchange needs no wait packet in the compute queue)
+        HpScope hp_q(HP_GQ);
+        need = hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess;
+    }
+    if (need) {
         HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
         // factor groups already forked: the other groups' launches write their factors' rows
         // of the slot from their streams (a fork after this point inherits the wait)
