@@ -886,6 +886,10 @@ static void free_decomp(tk_decomp* dc) {
 }
 
 // ------------------------------------------------------------------ reduce hand-off self-check
+// (Since round 5 the separate one-sweep Arnoldi reduce is a plain reduction: its readers
+// evaluate the scalars themselves.  What still hands values between the blocks of one launch is
+// the fused launch -- the reducers' values to the windows through the step word -- and the
+// one-sweep Lanczos reduce's last block; the check's job runs fused.)
 // k_reduce256 hands a one-sweep step's reduced values to the block that evaluates the next
 // step's scalars through agent-scope relaxed atomics -- correct on gfx950 by measurement
 // (/opt/skills/guides/MI355X_MICROARCH.md's hand-off table), not by the HIP memory model,
@@ -1060,6 +1064,9 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
             want = nf >= 2 && !(eg && atoi(eg) <= 1) && wins <= wmax;
         }
+        // (the hand-off self-check's own job: the fused launches are what hand values between
+        // the blocks of one launch -- the separate reduce is a plain reduction since round 5)
+        if (g_in_red_check) want = true;
         dc->fuse = method == TK_ARNOLDI && dc->onesweep && nf > 0 && want;
     }
     {
@@ -1542,6 +1549,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.redmm = 0;
     a.wseq = 0;
     a.werr = nullptr;
+    a.wsc = 0;
     return a;
 }
 
@@ -1676,8 +1684,11 @@ static tk_status red_flush(tk_decomp* dc) {
     const int j = dc->red_j;
     dc->red_j = -1;
     tk_ctx* c = dc->ctx;
+    // (a plain reduction: the fused windows and the bookkeeping evaluate the scalars)
+    KArgs rx = base_args(dc, j, 0);
+    rx.wsc = 1;
     if (!(dc->skip_mask & 1))
-        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, (j & 1) ? 5 : 1, 3 * j + 6, 0, c->stream, 0, j + 1), "reduce");
+        RUN(TCLS_RED, 2, launch_reduce(dc->df, dc->nf, (j & 1) ? 5 : 1, 3 * j + 6, 0, c->stream, 0, j + 1, &rx), "reduce");
     return TK_OK;
 }
 
@@ -1835,6 +1846,9 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // previous step's bookkeeping rides in a spare block of this launch, and this step's
         // is deferred the same way (tk_decomp_step completes the previous step's record).
         a.ubuf = j & 1;
+        // one stream: the reduce is a plain reduction and the windows evaluate the scalars;
+        // with factor groups the reduce's last block does (hidden behind the other group)
+        a.wsc = grouped ? 0 : 1;
         KArgs b = base_args(dc, -1, slot);
         b.j = -1;
         if (dc->bk_j >= 0 && dc->bk_j == j - 1 && dc->bk_kind == 0) b = dc->bk_args;
@@ -1897,7 +1911,7 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
             // (its last block per factor also evaluates the next step's scalars)
             if (!(dc->skip_mask & 1) && !dc->fuse) {
                 HpScope hp_(HP_RED);
-                RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1), "reduce");
+                RUN(TCLS_RED, 2, launch_reduce(dc->df, nf, 1, 3 * j + 6, 0, s, 0, j + 1, &a), "reduce");
             }
         }
         if (dc->fuse) dc->red_j = j;   // (reduced in the next launch, or by red_flush)

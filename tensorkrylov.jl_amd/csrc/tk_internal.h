@@ -117,6 +117,10 @@ struct KArgs {
     int redmm;        // ... with the memory-model hand-off (red_mm())
     unsigned long long wseq;   // ... and publish this in each factor's step word (DFac::rword)
     unsigned int* werr;        // ... a wait that gave up sets this (host-mapped)
+    // one-sweep Arnoldi, one stream (no factor groups): the step's reduce is a plain reduction and
+    // the windows evaluate the next step's scalars (d1_scalars); 0: the reduce's last block does
+    // and stores them (with two group streams that reduce hides behind the other group's sweep)
+    int wsc;
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register

@@ -132,6 +132,34 @@ __device__ __forceinline__ double row16_sum(double s) {
     s += dpp<0x121>(s);   // row_ror:1
     return s;
 }
+// lane 0's value in every lane (the rotations leave each lane its own rounding of the total)
+__device__ __forceinline__ double lane0(double x) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), 0),
+                            __builtin_amdgcn_readlane(__double2loint(x), 0));
+}
+// A one-sweep Arnoldi step's scalars from the previous step's reduced dots (RED1 = c [0,J) |
+// q [J,2J) | |u|^2 | <u,z> ..., J <= 64): beta = sqrt(|u|^2 - |c|^2), ib = 1/beta,
+// t1 = (<u,z> - c.q) ib (gamma = t1 ib, the coefficient of v_J in u_{J+1}).  One full wave,
+// lane l holding c[l], q[l] (zero for l >= J), a fixed-order butterfly and lane 0's sums: every
+// caller -- each window block of k_arn_d1 and the step's bookkeeping -- gets the same bits, so
+// no block has to hand them to the others (round 5: the reduce is a plain reduction).
+__device__ __forceinline__ void d1_scalars(double c0, double q0, double uu, double uz, double& beta, double& ib,
+                                           double& t1) {
+#pragma clang fp contract(off)
+    double cc = c0 * c0, cq = c0 * q0;
+    cc = row16_sum(cc);
+    cc += __shfl_xor(cc, 16);
+    cc += __shfl_xor(cc, 32);
+    cq = row16_sum(cq);
+    cq += __shfl_xor(cq, 16);
+    cq += __shfl_xor(cq, 32);
+    cc = lane0(cc);
+    cq = lane0(cq);
+    const double bsq = uu - cc;
+    beta = sqrt(bsq > 0.0 ? bsq : 0.0);
+    ib = 1.0 / beta;
+    t1 = (uz - cq) * ib;
+}
 
 // Reduce-scatter over each 16-lane row: lane l returns the sum over its row's 16 lanes of
 // x[l & 15].  Four exchange steps (partners l^8 by row_ror:8, l^7 by row_half_mirror, l^2
@@ -1069,9 +1097,13 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // loads, wait for the factor's step word, and read the coefficients the reducers produced in
     // this launch through sc1 vector loads; partials alternate between P1 / P1b by step parity
     constexpr bool VC = MODE & 1, FUSE = (MODE & 2) != 0;
+    // Bit 2 (WSC, one stream only): the previous step's reduce was a plain reduction -- wave 0
+    // evaluates the step's scalars (d1_scalars) and hands them to the block through LDS
+    constexpr bool WSC = (MODE & 4) != 0 && !FUSE;
     static_assert(!FUSE || LC == 0, "fused launches keep the whole register row in VGPRs");
     static_assert(LC % 8 == 0 && (LC == 0 || LC <= MAXC - 8), "LDS columns: whole chunks of 8, below the patched pairs");
     __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
+    __shared__ double d1s[WSC ? 2 : 1];                // the step's ib, gamma (wave 0 -> the block)
 #if TK_D1_COEF_LDS
     __shared__ __attribute__((aligned(16))) double cl[2][MAXC];   // c, h1
 #endif
@@ -1185,28 +1217,60 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // VC: the basis row through the caches (default policy) -- the launcher's choice when
         // this rank's per-step working set fits the 256 MiB Infinity Cache, so the next step
         // re-reads it from there; nt otherwise (streamed once, never re-read in time)
+        // the step's scalars come from the previous step's reduced dots (RED1 = [c (j) | q (j) |
+        // |u|^2, <u,z>, ..]): lane l loads c[l], q[l] ahead of the row (vmcnt lets these land
+        // first) and every wave evaluates them (d1_scalars); step 0 reads the init's
+        const int l = t & 63;
+        double cl0 = 0.0, ql0 = 0.0;
+        if constexpr (!FUSE) {
+            // (wave 0 evaluates them for the block and hands them on through LDS at the barrier
+            // before the SpMV, the first place that needs them: one 1 KB load per block)
+            if (WSC && j > 0 && t < 64 && l < j) {
+                cl0 = ld(d.RED1, l);
+                ql0 = ld(d.RED1, j + l);
+            }
+        }
         R.template loadm_even<LC / 2, VC ? 0 : 2>(tv, toff, jl);
         // (both loads issued before the patch below waits for the row)
         const double up = inb ? ld(Uin, r) : 0.0;
         const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
         if (j & 1) R.set_col(j - 1, e);
-        // the step's scalars, evaluated by the last block of the previous step's reduce
-        // (k_reduce256): RED1 = [c (j) | q (j) | |u|^2, <u,z>, .. (3j+3 values) | ib, gamma, ..]
+        // (step 0: ib, gamma of the init, k_post; with factor groups the reduce's last block
+        // stored them after the values)
         const double* s1 = d.RED1 + (j > 0 ? 3 * j + 3 : 2);
         double inv_beta, gamma;
         double sc, sq;
         if constexpr (FUSE) {
             // (the row loads above are in flight while the reducers of this launch finish)
             if (a.red) fuse_wait(d.rword, a.wseq, a.werr);
-            inv_beta = ld_ag(s1 + D1S_IB);
-            gamma = ld_ag(s1 + D1S_GAMMA);
             // lane l holds c[l] and q[l]; row_dot2_rl broadcasts them column by column (the same
             // values and FMA order as the scalar-cache form: bitwise the same sums)
-            const int l = t & 63;
-            row_dot2_rl<MAXC>(R, ld_ag(d.RED1 + l), ld_ag(d.RED1 + j + l), sc, sq);
+            const double hl = ld_ag(d.RED1 + l), gl = ld_ag(d.RED1 + j + l);
+            if (j > 0) {
+                double beta, t1;
+                d1_scalars(l < j ? hl : 0.0, l < j ? gl : 0.0, ld_ag(d.RED1 + 2 * j), ld_ag(d.RED1 + 2 * j + 1), beta,
+                           inv_beta, t1);
+                gamma = t1 * inv_beta;
+            } else {
+                inv_beta = ld_ag(s1 + D1S_IB);
+                gamma = ld_ag(s1 + D1S_GAMMA);
+            }
+            row_dot2_rl<MAXC>(R, hl, gl, sc, sq);
         } else {
-            inv_beta = CP4(s1)[D1S_IB];
-            gamma = CP4(s1)[D1S_GAMMA];
+            if (WSC && j > 0) {
+                inv_beta = gamma = 0.0;   // (from d1s after the barrier below)
+                if (t < 64) {
+                    double beta, ib, t1;
+                    d1_scalars(cl0, ql0, CP4(d.RED1)[2 * j], CP4(d.RED1)[2 * j + 1], beta, ib, t1);
+                    if (t == 0) {
+                        d1s[0] = ib;
+                        d1s[1] = t1 * ib;
+                    }
+                }
+            } else {
+                inv_beta = CP4(s1)[D1S_IB];
+                gamma = CP4(s1)[D1S_GAMMA];
+            }
 #if TK_D1_COEF_LDS
         row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sq);
 #else
@@ -1226,13 +1290,25 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // (the Hbar c terms cancel): the SpMV is applied to u_j itself, no Hbar is needed
         double* xv = xs[par];
         double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
-        const double vj = ok ? (up - sc) * inv_beta : 0.0;
 #if TK_BK_TEST & 32
+        if (WSC && j > 0) __syncthreads();
+        if (WSC && j > 0) inv_beta = d1s[0], gamma = d1s[1];
+        const double vj = ok ? (up - sc) * inv_beta : 0.0;
         xv[t] = vj;
-#else
-        xv[t] = up;
-#endif
         __syncthreads();
+#else
+        double vj = 0.0;
+        if constexpr (!WSC) vj = ok ? (up - sc) * inv_beta : 0.0;
+        xv[t] = up;
+        __syncthreads();
+        if constexpr (WSC) {
+            if (j > 0) {
+                inv_beta = d1s[0];
+                gamma = d1s[1];
+            }
+            vj = ok ? (up - sc) * inv_beta : 0.0;
+        }
+#endif
         const double au = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
         const double u = ok ? inv_beta * (au - sq) - gamma * vj : 0.0;
         D1_PHASE(1);
@@ -2057,16 +2133,19 @@ __global__ __launch_bounds__(1024) void k_red_lan(const DFac* __restrict__ F, KA
     lan_step_record(d, ax, (int)blockIdx.x, red[0], red[2], red[3], red[4], red[5], al_est, [](int) { return 0.0; });
 }
 
-// coefJ >= 0: one-sweep Arnoldi step (the last block evaluates the next step's scalars);
+// coefJ >= 0: one-sweep Arnoldi step -- a plain reduction into RED1 (its readers evaluate the
+// next step's scalars from it themselves, d1_scalars; round 4's last block that evaluated and
+// handed them on cost C4's one-factor step ~2 us);
 // RED_LAN: one-sweep Lanczos step (nv = 6 + j; 6 for factors without a Gram row; the last
 // block evaluates alpha, beta and writes the step's record, ax = the step's KArgs).
 // MM: the hand-off in the HIP memory model's own form (release/acquire add + acquire fence);
 // otherwise the measured relaxed form -- chosen per process by red_mm() (tk_abi.cpp's startup
 // self-check compares the two and keeps MM if they ever differ)
-// FUSED (a fused one-sweep launch's leading blocks, k_arn_d1 with a pending reduce): the last
-// block stores the scalars with agent-scope atomics, waits for them, then publishes `wseq` in the
-// factor's step word -- the in-launch hand-off row of /opt/skills/guides/MI355X_MICROARCH.md
-// (every store of the handed-off bytes sc1 and drained before the flag, every load of them sc1).
+// FUSED (a fused one-sweep launch's leading blocks, k_arn_d1 with a pending reduce): every
+// value is stored with an agent-scope atomic and drained before the block counts its arrival;
+// the last block publishes `wseq` in the factor's step word -- the in-launch hand-off row of
+// /opt/skills/guides/MI355X_MICROARCH.md (every store of the handed-off bytes sc1 and drained
+// before the flag, every load of them sc1).
 // which: 1 P1 -> RED1, 2 P2 -> RED2, 3 P1 -> RED2, 5 P1b -> RED1 (the odd steps' partials of a
 // fused handle).
 template <bool MM, bool FUSED>
@@ -2074,7 +2153,7 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
                                              const KArgs& ax, unsigned long long wseq) {
     __shared__ double rs[16];
     __shared__ int last;
-    const int nvs = nv;   // (the scalars' place after the values)
+    const int nv0 = nv;   // (the stored scalars' place after the values)
     if (coefJ == RED_LAN && !d.track_gram) nv = 6;
     if (coefJ >= 0 && !d.track_gram) nv = 2 * coefJ + 4;   // one-sweep Arnoldi: no Gram row
     if (c >= nv) return;
@@ -2099,8 +2178,8 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
         double r = 0.0;
 #pragma unroll
         for (int q = 0; q < 16; ++q) r += rs[q];
-        if (coefJ < 0 && coefJ != RED_LAN) {
-            st(which == 1 ? d.RED1 : d.RED2, c, r);
+        if ((coefJ < 0 && coefJ != RED_LAN) || (coefJ >= 0 && !FUSED && ax.wsc)) {
+            st(which == 1 || which == 5 ? d.RED1 : d.RED2, c, r);
         } else {
             // one-sweep step: publish the value coherently (agent-scope store, through to the
             // device-coherent level; its completion awaited), then count the arrival -- no
@@ -2125,7 +2204,7 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
             }
         }
     }
-    if (coefJ < 0 && coefJ != RED_LAN) return;
+    if ((coefJ < 0 && coefJ != RED_LAN) || (coefJ >= 0 && !FUSED && ax.wsc)) return;
     // (the one-sweep Lanczos' alpha estimate, read before the barrier: thread 0 of the last
     // block overwrites it below)
     const double al_est = coefJ == RED_LAN ? ld(d.sc, SC_ALPHA) : 0.0;
@@ -2139,45 +2218,31 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
                         [&](int c) { return cld(6 + c); });
         return;
     }
-    if (t >= 64) return;
-    // the next step's scalars from this step's dots (RED1 = c [0,J) | q [J,2J) | |u|^2 |
-    // <u,z> ..., J = coefJ <= 65): beta = sqrt(|u|^2 - |c|^2), ib = inv(beta),
-    // t1 = (<u,z> - c.q) ib, gamma = t1 ib = <v_J, A v_J> + (Hbar c)_J ib (the coefficient of
-    // v_J in u_{J+1}).  One wave, coherent loads, a fixed-order butterfly; k_arn_d1's blocks
-    // and the step's bookkeeping (bk_arn_d) read the results.
-    const int J = coefJ;
-    const double c0 = t < J ? cld(t) : 0.0, q0 = t < J ? cld(J + t) : 0.0;
-    const double c1 = t + 64 < J ? cld(t + 64) : 0.0, q1 = t + 64 < J ? cld(J + 64 + t) : 0.0;
-    const double uu = cld(2 * J), uz = cld(2 * J + 1);
-    double cc = fma(c1, c1, c0 * c0), cq = fma(c1, q1, c0 * q0);
-    cc = row16_sum(cc);
-    cc += __shfl_xor(cc, 16);
-    cc += __shfl_xor(cc, 32);
-    cq = row16_sum(cq);
-    cq += __shfl_xor(cq, 16);
-    cq += __shfl_xor(cq, 32);
-    if (t == 0) {
-        const double bsq = uu - cc;
-        const double beta = sqrt(bsq > 0.0 ? bsq : 0.0);
-        const double ib = 1.0 / beta;
-        const double t1 = (uz - cq) * ib;
-        double* o = d.RED1 + nvs;
-        if constexpr (FUSED) {
-            st_wt(o, D1S_IB, ib);
-            st_wt(o, D1S_GAMMA, t1 * ib);
-            st_wt(o, D1S_BETA, beta);
-            st_wt(o, D1S_T1, t1);
-        } else {
+    if constexpr (!FUSED) {
+        // one-sweep Arnoldi with factor groups: the last block evaluates the next step's scalars
+        // (d1_scalars, J = coefJ <= 64) and stores them after the values for the windows and
+        // the bookkeeping (the same bits as evaluating them there)
+        if (t >= 64) return;
+        const int J = coefJ;
+        double beta, ib, t1;
+        d1_scalars(t < J ? cld(t) : 0.0, t < J ? cld(J + t) : 0.0, cld(2 * J), cld(2 * J + 1), beta, ib, t1);
+        if (t == 0) {
+            double* o = d.RED1 + nv0;
             st(o, D1S_IB, ib);
             st(o, D1S_GAMMA, t1 * ib);
             st(o, D1S_BETA, beta);
             st(o, D1S_T1, t1);
+            __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        return;
+    }
+    // FUSED one-sweep Arnoldi: every value is through to the device (each block drained its
+    // store before counting): publish the step (ctr's reset is ordered before the next launch
+    // by the kernel boundary)
+    if (t == 0) {
         __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if constexpr (FUSED) {
-            __builtin_amdgcn_s_waitcnt(0);   // (the scalars and the values are through to the device)
-            __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 template <bool MM>
@@ -2324,8 +2389,14 @@ __device__ void bk_arn_d(const DFac& d, const KArgs& a, double* rec, double* lds
     for (int i = t; i < nv; i += TPB) red[i] = ld_ag(d.RED1 + i);
     for (int i = t; i <= j; i += TPB) Hs[j * J2 + i] = ld(d.g, i);
     const double bnorm = ld(d.sc, SC_BNORM);
-    const double beta = ld_ag(d.RED1 + nv + D1S_BETA), ib = ld_ag(d.RED1 + nv + D1S_IB), t1 = ld_ag(d.RED1 + nv + D1S_T1);
     __syncthreads();
+    // the step's scalars, evaluated here as the next step's windows evaluate them (d1_scalars:
+    // the same bits); RED1 = c [0,J) | q [J,2J) | |u|^2 | <u,z>, J = j + 1
+    double beta, ib, t1;
+    {
+        const int l = t & 63, J = j + 1;
+        d1_scalars(l < J ? red[l] : 0.0, l < J ? red[J + l] : 0.0, red[2 * J], red[2 * J + 1], beta, ib, t1);
+    }
     for (int i = t; i <= j; i += TPB) {
         const double ci = red[i];
         const double hv = Hs[j * J2 + i] + ci;
@@ -3089,6 +3160,9 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
             if (fuse) {
                 if (vcache) hipLaunchKernelGGL((k_arn_d1<MV, FV, 3>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
                 else hipLaunchKernelGGL((k_arn_d1<MV, FV, 2>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+            } else if (a.wsc) {
+                if (vcache) hipLaunchKernelGGL((k_arn_d1<MV, FV, 5>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
+                else hipLaunchKernelGGL((k_arn_d1<MV, FV, 4>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
             } else {
                 if (vcache) hipLaunchKernelGGL((k_arn_d1<MV, FV, 1>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
                 else hipLaunchKernelGGL((k_arn_d1<MV, FV, 0>), dim3(gx, nf), dim3(TPB), lds, s, F, a, b);
