@@ -842,6 +842,12 @@ struct tk_decomp {
     // per-slot events: compute -> exchange (slot written) and exchange -> compute
     // (the all-reduce has finished reading the slot's send rows)
     std::vector<hipEvent_t> ev_c, ev_x;
+    // slot guards: how often each ev_x was recorded, and the (event, record) the compute stream
+    // last waited for -- the slots of one exchange share its event, so one wait packet covers
+    // them all (a barrier packet per step cost the host-ahead bench sweeps ~2-3 us per step)
+    std::vector<unsigned> ev_x_gen;
+    int guard_ev = -1;
+    unsigned guard_gen = 0;
 };
 
 int tk_record_len(int kmax) { return rec_len(kmax); }
@@ -1347,6 +1353,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             }
         }
         dc->xslot_seq.assign(kmax + 2, 0);
+        dc->ev_x_gen.assign(kmax + 2, 0);
         dc->xcnt.assign(kmax + 2, 0);
         dc->xev.resize(kmax + 2);
         for (int i = 0; i < kmax + 2; ++i) dc->xev[i] = i;
@@ -1491,7 +1498,11 @@ static tk_status slot_guard(tk_decomp* dc, int slot) {
         HpScope hp_q(HP_GQ);
         need = hipEventQuery(dc->ev_x[dc->xev[slot]]) != hipSuccess;
     }
+    const int ei = dc->xev[slot];
+    if (need && ei == dc->guard_ev && dc->ev_x_gen[ei] == dc->guard_gen) need = false;   // (waited already)
     if (need) {
+        dc->guard_ev = ei;
+        dc->guard_gen = dc->ev_x_gen[ei];
         HIPCHK(hipStreamWaitEvent(dc->ctx->stream, dc->ev_x[dc->xev[slot]], 0));
         // factor groups already forked: the other groups' launches write their factors' rows
         // of the slot from their streams (a fork after this point inherits the wait)
@@ -1601,6 +1612,7 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
         NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
     }
     HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));
+    ++dc->ev_x_gen[s1];
     for (int sl = s0; sl <= s1; ++sl) dc->xev[sl] = s1;
     if (dc->xdone) {
         ++dc->seq;
