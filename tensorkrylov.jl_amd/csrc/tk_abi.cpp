@@ -1608,13 +1608,22 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
             launch_delay_us(delay_us, c->xstream);
             LAUNCHCHK("xch delay");
         }
+        // TKHIP_TEST_XCH_SKIP (timing only, wrong records): 1 no mirror kernel, 2 no all-reduce
+        static const int xskip = [] {
+            const char* e = getenv("TKHIP_TEST_XCH_SKIP");
+            return e ? atoi(e) : 0;
+        }();
         HpScope hp_n(HP_NCCL);
-        NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
+        if (!(xskip & 2)) NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
     }
     HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));
     ++dc->ev_x_gen[s1];
     for (int sl = s0; sl <= s1; ++sl) dc->xev[sl] = s1;
-    if (dc->xdone) {
+    static const bool nomirror = [] {
+        const char* e = getenv("TKHIP_TEST_XCH_SKIP");
+        return e && (atoi(e) & 1);
+    }();
+    if (dc->xdone && !nomirror) {
         ++dc->seq;
         for (int sl = s0; sl <= s1; ++sl) dc->xslot_seq[sl] = dc->seq;
         HpScope hp_m(HP_MIRROR);
