@@ -795,11 +795,12 @@ struct tk_decomp {
     // exchange stream waits (hipStreamWaitValue64) for xcount
     unsigned long long* xflag = nullptr;
     unsigned long long xcount = 0;
-    // factor groups under an exchange: one signal word per local factor (DFac::xsig, its value
-    // at create in xsig0); a slot is complete when every factor's word shows xscnt[slot] steps
+    // records exchange: one signal word per local factor (DFac::xsig, zeroed at create), set
+    // by each step's k_post / bookkeeping block to the step's xval; a slot is complete when every
+    // factor's word shows xscnt[slot]
     std::vector<unsigned long long*> xsig;
-    std::vector<unsigned long long> xsig0, xscnt;
-    unsigned long long xstep = 0;
+    std::vector<unsigned long long> xscnt;   // per slot: the xval of the step that writes it
+    unsigned long long xsq = 0, cur_xval = 0;
     // TKHIP_TEST_GROUP_DELAY_US (tests, read at create): group 0's stream held back this long
     // before each grouped launch, so the other groups run steps ahead of it
     double gdelay_us = 0.0;
@@ -1264,11 +1265,41 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         (void)hipGetLastError();   // an unsupported signal path must not leave a sticky error
     }
     dc->slot_seq.assign(kmax + 2, 0);
+    if (dc->recv != dc->rec && dc->xflag) {
+        // one signal word per local factor (signal memory is host memory): each step's k_post /
+        // bookkeeping block stores the step's KArgs::xval there -- a posted store where an add was
+        // a round trip the launch waited for -- and the exchange waits for every word
+        // (exchange_range).  Allocation failure: the one shared word with adds
+        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");
+        bool okw = !(esh && esh[0] == '1');
+        for (int f = 0; okw && f < nf; ++f) {
+            void* p = nullptr;
+            const unsigned long long zero = 0;
+            okw = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p;
+            if (okw) {
+                dc->xsig.push_back((unsigned long long*)p);
+                okw = hipMemcpy(p, &zero, 8, hipMemcpyHostToDevice) == hipSuccess;
+            }
+        }
+        for (int f = 0; okw && f < nf; ++f) dc->hf[f].xsig = dc->xsig[f];
+        okw = okw && hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) == hipSuccess;
+        if (!okw) {
+            for (unsigned long long* p : dc->xsig) hipFree(p);
+            dc->xsig.clear();
+            for (int f = 0; f < nf; ++f) dc->hf[f].xsig = nullptr;
+            if (hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) != hipSuccess) {
+                free_decomp(dc);
+                return fail(TK_ERR_HIP, "upload descriptors");
+            }
+        }
+        dc->xscnt.assign(kmax + 2, 0);
+        (void)hipGetLastError();
+    }
     {
-        // with a records exchange the groups need the signal word: the exchange of a step's
-        // slot then waits for the count both groups' bookkeeping blocks add (an event marker
-        // would sit in one group's stream only), and every slot guard is waited for on both
-        // group streams (slot_guard)
+        // with a records exchange the groups need the per-factor signal words: the exchange of
+        // a step's slot then waits for every factor's word (an event marker would sit in one
+        // group's stream only), and every slot guard is waited for on both group streams
+        // (slot_guard)
         // One-sweep Lanczos groups its Gram-free steps (k_lan_1w + k_red_lan) the same way:
         // each launch's bookkeeping blocks mirror and signal their own group's factors (host
         // words offset by the group's first factor), k_red_lan writes only device records
@@ -1284,35 +1315,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
                   hipEventCreateWithFlags(&dc->fev_fork, hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
         for (int g = 0; ok && g < G - 1; ++g)
             ok = hipEventCreateWithFlags(&dc->fev_join[g], hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
-        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");   // (diagnostics: the round-4 shared word)
-        if (ok && dc->recv != dc->rec && !(esh && esh[0] == '1')) {
-            // the groups' streams run apart (one may be a step ahead of another), so a shared
-            // count can be reached with a step of one group missing: each factor signals its
-            // own word and the exchange waits for every word (exchange_range)
-            for (int f = 0; ok && f < nf; ++f) {
-                void* p = nullptr;
-                unsigned long long v0 = 0;
-                ok = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p;
-                if (ok) {
-                    dc->xsig.push_back((unsigned long long*)p);
-                    ok = hipMemcpy(&v0, p, 8, hipMemcpyDeviceToHost) == hipSuccess;
-                }
-                dc->xsig0.push_back(v0);
-            }
-            for (int f = 0; ok && f < nf; ++f) dc->hf[f].xsig = dc->xsig[f];
-            ok = ok && hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) == hipSuccess;
-            if (!ok) {   // (no groups then: the one shared word)
-                for (unsigned long long* p : dc->xsig) hipFree(p);
-                dc->xsig.clear();
-                dc->xsig0.clear();
-                for (int f = 0; f < nf; ++f) dc->hf[f].xsig = nullptr;
-                if (hipMemcpy(dc->df, dc->hf.data(), nf * sizeof(DFac), hipMemcpyHostToDevice) != hipSuccess) {
-                    free_decomp(dc);
-                    return fail(TK_ERR_HIP, "upload descriptors");
-                }
-            }
-            dc->xscnt.assign(kmax + 2, 0);
-        }
+        // (factor groups under an exchange need the per-factor words; TKHIP_TEST_SHARED_XSIG=1,
+        // diagnostics only, runs them on the round-4 shared count)
+        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");
+        ok = ok && (dc->recv == dc->rec || !dc->xsig.empty() || (esh && esh[0] == '1'));
         if (ok) {
             dc->ngr = G;
             for (int g = 0; g <= G; ++g) dc->gst[g] = g * nf / G;
@@ -1561,6 +1567,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.wseq = 0;
     a.werr = nullptr;
     a.wsc = 0;
+    a.xval = 0;
     return a;
 }
 
@@ -1582,7 +1589,7 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
     if (dc->xflag && s0 >= 1 && s1 <= dc->kmax) {
         if (!dc->xsig.empty()) {   // (factor groups: every factor's own count)
             for (size_t f = 0; f < dc->xsig.size(); ++f)
-                HIPCHK(hipStreamWaitValue64(c->xstream, dc->xsig[f], dc->xsig0[f] + dc->xscnt[s1],
+                HIPCHK(hipStreamWaitValue64(c->xstream, dc->xsig[f], dc->xscnt[s1],
                                             hipStreamWaitValueGte, 0xFFFFFFFFFFFFFFFFull));
         } else {
             HIPCHK(hipStreamWaitValue64(c->xstream, dc->xflag, dc->xcnt[s1], hipStreamWaitValueGte,
@@ -1687,11 +1694,11 @@ static double d1_cache_bytes() {
 
 // Step j's record is enqueued on this rank (its k_post, or the bookkeeping block of the
 // next k_arn_d1): count its signal and note its host sequence number.  Local only.
-static void complete_step(tk_decomp* dc, int j, unsigned long long seqj) {
+static void complete_step(tk_decomp* dc, int j, unsigned long long seqj, unsigned long long xvalj) {
     if (dc->xflag) dc->xcount += (unsigned long long)dc->nf;   // one add per factor
     if (dc->hdone) dc->slot_seq[j + 1] = seqj;
     dc->xcnt[j + 1] = dc->xcount;
-    if (!dc->xsig.empty()) dc->xscnt[j + 1] = ++dc->xstep;
+    if (!dc->xsig.empty()) dc->xscnt[j + 1] = xvalj;
     dc->xs.complete(j + 1);
 }
 
@@ -1727,7 +1734,7 @@ static tk_status bk_flush(tk_decomp* dc) {
     const KArgs ax = dc->bk_args;
     dc->bk_j = -1;
     RUN(TCLS_RED, 2, launch_post(dc->df, dc->nf, ax, dc->bk_kind ? POST_SIGNAL : POST_ARN_D, 0, 1, s), "post");
-    complete_step(dc, j, ax.seq);
+    complete_step(dc, j, ax.seq, ax.xval);
     return TK_OK;
 }
 
@@ -1779,7 +1786,6 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     // a new sequence: slots of the previous one that never went out are dropped (on every rank)
     dc->xs.reset();
     dc->xcnt[0] = dc->xcount;
-    if (!dc->xsig.empty()) dc->xscnt[0] = dc->xstep;
     dc->xs.complete(0);
     if (dc->recv != dc->rec) {
         st = xsend(dc, dc->xs.need(0));
@@ -1838,6 +1844,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
     KArgs a = base_args(dc, j, slot);
     KArgs ax = a;          // the step's last k_post signals the exchange stream / the host
     ax.xflag = dc->xflag;
+    ax.xval = ++dc->xsq;
+    dc->cur_xval = ax.xval;
     const bool hsig = dc->hdone != nullptr;
     dc->slot_seq[slot] = 0;
     if (hsig) {
@@ -2078,7 +2086,7 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     HIPCHK(hipSetDevice(dc->ctx->device));
     HpScope hp_step(HP_STEP);
     const int prev_bk = dc->bk_j;
-    const unsigned long long prev_seq = dc->bk_args.seq;
+    const unsigned long long prev_seq = dc->bk_args.seq, prev_xval = dc->bk_args.xval;
     tk_status st = j == dc->fail_step ? fail(TK_ERR_HIP, "step %d: injected failure (TKHIP_TEST_FAIL_STEP)", j)
                                       : step_impl(dc, j, rec_out);
     if (st) {
@@ -2091,13 +2099,13 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     if (dc->bk_j == j) {
         // one sweep: this launch carried step j-1's bookkeeping (its record is complete);
         // step j's own waits for the next launch unless the caller wants it now
-        if (prev_bk == j - 1 && prev_bk >= 0) complete_step(dc, prev_bk, prev_seq);
+        if (prev_bk == j - 1 && prev_bk >= 0) complete_step(dc, prev_bk, prev_seq, prev_xval);
         if (rec_out || !dc->bk_fold) {
             st = bk_flush(dc);
             if (st) return st;
         }
     } else {
-        complete_step(dc, j, dc->seq);
+        complete_step(dc, j, dc->seq, dc->cur_xval);
     }
     if (dc->recv != dc->rec) {
         // canonical: slots <= j are written on every rank now; full groups go out

@@ -84,9 +84,10 @@ struct DFac {
     // steps' partials, and the step word the reducers publish and the window blocks wait for
     double* P1b;
     unsigned long long* rword;
-    // factor groups under a records exchange: this factor's own exchange signal word (the
-    // groups' streams run apart, so one shared count could be reached with a step of one group
-    // missing and another group's next step counted instead); null: KArgs::xflag
+    // records exchange: this factor's own exchange signal word, set to the step's KArgs::xval by
+    // a plain store (host-resident signal memory: an atomic add there is a non-posted round trip
+    // the launch waits for; with factor groups one shared count could also be reached with a
+    // step of one group missing); null: an add to KArgs::xflag
     unsigned long long* xsig;
 };
 
@@ -108,6 +109,8 @@ struct KArgs {
                                  // ([d_total][m]); k_post copies its row there ...
     unsigned long long* hdone;   // ... then stores `seq` to hdone[local factor] (host-mapped)
     unsigned long long seq;
+    unsigned long long xval;     // exchange signal of this step (per-factor words, DFac::xsig): the
+                                 // value its k_post / bookkeeping block stores (monotonic per handle)
     int ecol;         // flush of the one-sweep pending column: this column (j) is in DFac::E, not V (-1: none)
     int mfs;          // CGS2 pass 1: A U comes from DFac::AU (k_spmv_mf ran), not from its own gathers
     int sl;           // 1: V in single-column tiles (column c of a tile at c * 256 doubles, row

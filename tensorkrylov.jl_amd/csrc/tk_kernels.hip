@@ -2458,7 +2458,10 @@ __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirror
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (a.xflag) __hip_atomic_fetch_add(d.xsig ? d.xsig : a.xflag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (a.xflag) {
+                if (d.xsig) __hip_atomic_store(d.xsig, a.xval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                else __hip_atomic_fetch_add(a.xflag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             if (a.hdone) __hip_atomic_store(a.hdone + fidx, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         return;
@@ -2475,7 +2478,10 @@ __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirror
     }
     if (threadIdx.x == 0) {
         __threadfence_system();
-        if (a.xflag) atomicAdd_system(d.xsig ? d.xsig : a.xflag, 1ull);
+        if (a.xflag) {
+            if (d.xsig) __hip_atomic_store(d.xsig, a.xval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            else atomicAdd_system(a.xflag, 1ull);
+        }
         if (a.hdone)
             __hip_atomic_store(a.hdone + fidx, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
