@@ -834,6 +834,13 @@ struct tk_decomp {
     std::vector<void*> allocs;
     double* rec = nullptr;   // send records [(kmax+2) slots][d_total][m] (local rows only)
     double* recv = nullptr;  // all-reduced records (== rec on a single rank)
+    // multi-rank: the send rows alternate between two buffers by sequence (tk_decomp_init
+    // swaps rec / rec_alt and the slot-guard state with them), so a sequence's steps never
+    // wait for the previous sequence's all-reduces to finish reading their rows -- only the
+    // ones of two sequences back, long done unless the host runs a whole sequence ahead
+    double* rec_alt = nullptr;
+    std::vector<unsigned long long> xslot_seq_alt;
+    std::vector<int> xev_alt;
     // replica of factors another rank owns (exp-sum-term split, tk_decomp_set_replica): the
     // all-reduce sends these zero rows instead of rec, so every record is counted once
     double* zrec = nullptr;
@@ -1225,9 +1232,10 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     if (const char* eb = getenv("TKHIP_BK_FOLD")) dc->bk_fold = eb[0] != '0';
     dc->bk_fold = dc->bk_fold && TK_D1_ONEWIN;   // (the window-loop kernel has no bookkeeping blocks)
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
-    if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1')))
+    if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1'))) {
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
-    else
+        DA(dc->rec_alt, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
+    } else
         dc->recv = dc->rec;
 #undef DA
     if (dc->recv != dc->rec) {
@@ -1363,6 +1371,8 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->xcnt.assign(kmax + 2, 0);
         dc->xev.resize(kmax + 2);
         for (int i = 0; i < kmax + 2; ++i) dc->xev[i] = i;
+        dc->xslot_seq_alt = dc->xslot_seq;
+        dc->xev_alt = dc->xev;
         if (const char* eg = getenv("TKHIP_XCH_GROUP")) dc->xs.group = std::min(64, std::max(1, atoi(eg)));
         if (const char* es = getenv("TKHIP_TEST_XCH_STALL")) {
             void* p = nullptr;
@@ -1765,6 +1775,16 @@ tk_status tk_decomp_init(tk_decomp* dc, double* rec_out) { TK_API_BEGIN
     if (dc->gram_inflight) {   // (a Gram of the previous sequence still reads the basis)
         HIPCHK(hipStreamWaitEvent(s, dc->gev_done, 0));
         dc->gram_inflight = false;
+    }
+    static const bool rec_alt_on = [] {   // (TKHIP_REC_ALT=0: one send buffer, A/B)
+        const char* e = getenv("TKHIP_REC_ALT");
+        return !(e && e[0] == '0');
+    }();
+    if (dc->rec_alt && rec_alt_on && dc->xslot_seq.size() == dc->xslot_seq_alt.size()) {
+        // (the other send buffer: its last readers are the previous-but-one sequence's)
+        std::swap(dc->rec, dc->rec_alt);
+        std::swap(dc->xslot_seq, dc->xslot_seq_alt);
+        std::swap(dc->xev, dc->xev_alt);
     }
     st = slot_guard(dc, 0);
     if (st) return st;

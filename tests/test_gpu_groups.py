@@ -150,6 +150,50 @@ def test_factor_groups_exchange_waits_for_every_group(ctx, fuse, monkeypatch):
         c2.close()
 
 
+@pytest.mark.parametrize("alt", ["0", "1"])
+def test_back_to_back_sequences_under_records_exchange(ctx, alt, monkeypatch):
+    """Sequences issued back to back on one exchange handle, the host running ahead (group 0
+    held back, no records read between the second and third sequence): the send rows alternate
+    between two buffers by sequence (TKHIP_REC_ALT, default on), the slot guards tracking each
+    buffer's last all-reduce.  Every sequence's exchanged records equal the local run bit for
+    bit -- the zero-initialised second buffer read before its rows were written would show as
+    zero rows."""
+    import tkamd as tk
+    d, n, K = 3, 1 << 14, 24
+    monkeypatch.setenv("TKHIP_REC_ALT", alt)
+    rng = np.random.default_rng(21)
+    mat = tk.assemble_matrix(n, "ConvDiff")
+    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+
+    def run(c, G):
+        monkeypatch.setenv("TKHIP_FACTOR_GROUPS", G)
+        A = tk.DeviceMatrix(c, mat)
+        dev = tk.DeviceDecomposition(c, 0, d, 0, [A] * d, bs, K)
+        out = []
+        for seq in range(4):
+            dev.init(False)
+            dev.sweep(0, K)
+            if seq != 1:
+                out.append(dev.records(0, K + 1))
+        dev.close()
+        A.close()
+        return out
+
+    local = run(ctx, "1")
+    assert all(np.array_equal(local[0], r) for r in local[1:])
+    c2 = tk.Context(0)
+    c2.init_comm(tk.unique_id(), 1, 0)
+    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
+    monkeypatch.setenv("TKHIP_TEST_GROUP_DELAY_US", "100")
+    try:
+        for G in ("1", "2"):
+            for r in run(c2, G):
+                assert np.array_equal(local[0], r)
+    finally:
+        monkeypatch.delenv("TKHIP_TEST_GROUP_DELAY_US")
+        c2.close()
+
+
 @pytest.mark.parametrize("d", [2, 5])
 def test_lanczos_factor_groups_bitwise_equal_one_stream(ctx, d, monkeypatch):
     """One-sweep TensorLanczos without Gram rows (k_lan_1w + k_red_lan, the deferred Gram)
