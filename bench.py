@@ -18,7 +18,10 @@ Factors are partitioned over ranks (one process per GPU): the total work is fixe
 the scaling is STRONG (see DESIGN.md "Multi-GPU").
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config C1|C2|C3|C4]
-       (N > 1: launched by torch.distributed.run, one rank per GPU)
+       N > 1: one rank per GPU.  Either launch it under torch.distributed.run yourself, or run
+       `python bench.py --gpus N ...` and it starts `python -m torch.distributed.run
+       --nproc-per-node N ... bench.py <same args>` as a child process (before anything here
+       touches the GPU), passes rank 0's JSON line through and exits with the child's status.
 
 Multi-rank control plane: the RCCL unique id is handed from rank 0 to the others
 through a file keyed by the launcher's pid, and the barrier / max-over-ranks use RCCL
@@ -87,6 +90,39 @@ def alg_bytes_step(n, nnz, k, method="TensorArnoldi", sweeps=2, mat_bytes=None, 
     return b
 
 
+def launcher_argv(n, argv, port):
+    """The child command of a self-launched N-rank run: torch.distributed.run on this node,
+    one rank per GPU, rendezvous on 127.0.0.1, each rank running this file with the same
+    arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n, argv):
+    """`--gpus N` without a launcher: start the N ranks as a child (torch.distributed.run),
+    wait for it and return its exit status.  Nothing in this process has loaded the HIP
+    runtime or libtkhip (tkamd is imported only inside main's rank path), so the ranks own
+    the GPUs alone; the ranks' stdout -- rank 0's JSON line -- is this process's stdout."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    p = subprocess.Popen(launcher_argv(n, argv, _free_port()), env=env)
+    try:
+        return p.wait()
+    except KeyboardInterrupt:
+        p.terminate()
+        return p.wait()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -115,6 +151,9 @@ def main():
     ap.add_argument("--pmc-mode", action="store_true",
                     help="run exactly one untimed sweep (for rocprofv3 --pmc passes)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # (before tkamd is imported: the parent never maps the HIP runtime)
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     import tkamd
     from tkamd import _lib as L
@@ -123,8 +162,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("--gpus %d needs torch.distributed.run with %d ranks" % (args.gpus, args.gpus))
+        sys.exit("bench.py: --gpus %d but the launcher started %d rank(s) (WORLD_SIZE)" % (args.gpus, world))
 
     d, n, cls, method, K, inst = CONFIGS[args.config]
     if args.method:
@@ -397,6 +435,9 @@ def main():
             "value": round(value, 3),
             "unit": "iterations/s",
             "n_gpus": world,
+            "world": world,
+            # ranks RCCL joined (ncclCommCount; 0 = no communicator, the N = 1 run)
+            "rccl_nranks": ctx.comm_count(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * elapsed / args.steps, 3),
@@ -565,7 +606,9 @@ def cpu_baseline(csc, n, d, K, seconds):
 
 if __name__ == "__main__":
     try:
-        main()
+        rc = main()
+        if rc:
+            sys.exit(rc)
     except Exception as e:   # noqa: BLE001
         # a libtkhip error (e.g. TK_ERR_RCCL: a peer never joined an all-reduce within
         # TKHIP_WAIT_S) ends THIS rank with its diagnosis; exit without running destructors,

@@ -80,6 +80,9 @@ tk_status tk_comm_init(tk_ctx* ctx, const char id[128], int nranks, int rank);
 /* In-place sum all-reduce of `count` doubles of host memory through the device (test
  * and control-plane use; the hot path's exchange is internal to tk_decomp_step). */
 tk_status tk_comm_allreduce_host(tk_ctx* ctx, double* buf, size_t count);
+/* Ranks of ctx's communicator as RCCL reports them (ncclCommCount); 0 without one.
+ * bench.py reports it beside the launcher's WORLD_SIZE. */
+tk_status tk_comm_count(tk_ctx* ctx, int* nranks_out);
 
 /* ---------------------------------------------------------------- coefficient matrices */
 /* A_s as SparseMatrixCSC (src/tensor_struct.jl:48-68 assemble_matrix, stored in

@@ -414,6 +414,17 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_
     TK_API_END
 }
 
+tk_status tk_comm_count(tk_ctx* c, int* nranks_out) { TK_API_BEGIN
+    CHECKARG(c && nranks_out, "NULL argument");
+    *nranks_out = 0;
+    if (!c->comm) return TK_OK;
+    int n = 0;
+    NCCLCHK(ncclCommCount(c->comm, &n));
+    *nranks_out = n;
+    return TK_OK;
+    TK_API_END
+}
+
 // ------------------------------------------------------------------ matrices
 struct tk_mat {
     tk_ctx* ctx;

@@ -48,6 +48,7 @@ def lib():
         "tk_comm_unique_id": (I, [ctypes.c_char_p]),
         "tk_comm_init": (I, [P, ctypes.c_char_p, I, I]),
         "tk_comm_allreduce_host": (I, [P, DP, ctypes.c_size_t]),
+        "tk_comm_count": (I, [P, ctypes.POINTER(I)]),
         "tk_matrix_from_csc": (I, [P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), DP, I, ctypes.POINTER(P)]),
         "tk_matrix_from_csr": (I, [P, I64, ctypes.POINTER(I64), ctypes.POINTER(I64), DP, I, ctypes.POINTER(P)]),
         "tk_matrix_destroy": (I, [P]),
@@ -104,7 +105,7 @@ def lib():
 
 # every symbol include/tk.h declares (tests check the .so exports all of them)
 EXPORTS = ("tk_last_error", "tk_version", "tk_reduce_handoff", "tk_ctx_create", "tk_ctx_destroy", "tk_ctx_sync",
-           "tk_comm_unique_id", "tk_comm_init", "tk_comm_allreduce_host",
+           "tk_comm_unique_id", "tk_comm_init", "tk_comm_allreduce_host", "tk_comm_count",
            "tk_matrix_from_csc", "tk_matrix_from_csr", "tk_matrix_destroy", "tk_matrix_format", "tk_matvec",
            "tk_record_len", "tk_decomp_create", "tk_decomp_destroy", "tk_decomp_arnoldi_sweeps",
            "tk_decomp_exchange_signalled", "tk_decomp_set_replica", "tk_decomp_agree", "tk_decomp_next_step",

@@ -35,6 +35,12 @@ class Context:
         L.check(self._lib.tk_comm_allreduce_host(self.h, L.dptr(arr), arr.size))
         return arr
 
+    def comm_count(self):
+        """Ranks of the communicator as RCCL reports them (ncclCommCount); 0 without one."""
+        n = ctypes.c_int()
+        L.check(self._lib.tk_comm_count(self.h, ctypes.byref(n)))
+        return n.value
+
     def timing(self, level):
         L.check(self._lib.tk_timing_enable(self.h, int(level)))
 
