@@ -212,9 +212,15 @@ for (Name, method, orth) in ((:HIPTensorArnoldi, TK_ARNOLDI, :Arnoldi),
 end
 
 # tensorkrylov! needs nmax before the decomposition is built: record it, then run the
-# package's own driver unchanged.
+# package's own driver unchanged.  The signature is the reference's
+# (src/tensor_krylov_method.jl:36-43) with argument 6 narrowed to the HIP types and argument 7
+# typed exactly as there (mode::Type{<:Mode} = SilentMode): this method is then strictly more
+# specific than the reference's in every argument.  (An untyped `mode` made the 7-argument
+# call from the 6-argument default ambiguous -- more specific in argument 6, less in 7 -- and
+# solve_tensorized_system, src/system.jl:73-79, raised a MethodError on the first solve.)
 function tensorkrylov!(conv::ConvergenceData{T}, A::KronMat{matT, U}, b::KronProd{T}, tol::T, nmax::Int,
-                       t::Type{<:HIPTensorDecomposition}, mode = TensorKrylov.SilentMode) where {matT, T, U <: Instance}
+                       t::Type{<:HIPTensorDecomposition},
+                       mode::Type{<:TensorKrylov.Mode} = TensorKrylov.SilentMode) where {matT, T, U <: Instance}
     NMAX[] = nmax
     try
         return invoke(tensorkrylov!, Tuple{ConvergenceData{T}, KronMat{matT, U}, KronProd{T}, T, Int,
