@@ -37,6 +37,21 @@
 
 using namespace tk;
 
+// Test build (tests/_build/libtkhip_test.so: -DTK_TEST_BUILD=1, made by __graft_entry__.build()
+// for the test suite only).  The switches that skip work, drop guards or inject failures
+// (TKHIP_TEST_SKIP, _XCH_SKIP, _NO_GUARD, _SHARED_XSIG, _XCH_STALL, _FAIL_STEP, _FUSE_SPIN)
+// and the multi-process transport on one GPU (tk_comm_init_test) exist only there: in the
+// product library TEST_ENV is a constant NULL, so no environment variable can make
+// libtkhip.so produce wrong records.
+#ifndef TK_TEST_BUILD
+#define TK_TEST_BUILD 0
+#endif
+#if TK_TEST_BUILD
+#define TEST_ENV(name) getenv(name)
+#else
+#define TEST_ENV(name) ((const char*)nullptr)
+#endif
+
 // ------------------------------------------------------------------ host issue profile
 // TKHIP_HOST_PROFILE=1 (diagnostics): host time spent in each part of a step's issue, summed
 // over the process and printed to stderr at exit -- where the 8-15 us per step of
@@ -131,6 +146,7 @@ struct tk_ctx {
     hipStream_t gstream = nullptr;   // deferred orthogonality Gram (tk_decomp_gram), overlaps compute
     hipStream_t fstream = nullptr;   // the second factor group of one-sweep Arnoldi steps (tk_decomp)
     ncclComm_t comm = nullptr;
+    struct TestComm* tcomm = nullptr;   // test build: the shared-memory stand-in for RCCL
     int nranks = 1, rank = 0;
     int timing = 0;   // 0 off, 1 step level, 2 per kernel class
     std::vector<hipEvent_t> ev[TCLS_N];   // start/stop pairs
@@ -142,6 +158,10 @@ struct tk_ctx {
     // this device, so its buffers, streams and communicator are left to process exit
     bool stuck = false;
     std::vector<hipEvent_t> evpool;   // recycled timing events (no hipEventCreate per step)
+    // host-mapped error word of the fused one-sweep launches (k_arn_d1's bounded wait for its
+    // in-launch reducers gave up: that step's values are wrong).  Sticky; every call that
+    // hands results out after a device sync checks it (werr_check)
+    unsigned int* werr = nullptr;
     // Handles may be destroyed in any order (Julia finalizers, Python GC): matrices and
     // decompositions hold a reference on their context, decompositions on their matrices.
     std::atomic<int> refs{1};
@@ -208,7 +228,11 @@ static double wait_limit_s() {
     return v > 0 ? v : 120.0;
 }
 
+// a multi-rank communicator: RCCL, or (test build) the shared-memory stand-in
+static inline bool has_peers(const tk_ctx* c) { return c->comm != nullptr || c->tcomm != nullptr; }
+
 static const char* comm_state(tk_ctx* c) {
+    if (c->tcomm) return "test transport: a peer has not posted its contribution";
     if (!c->comm) return "no communicator";
     ncclResult_t r = ncclSuccess;
     if (ncclCommGetAsyncError(c->comm, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
@@ -234,7 +258,7 @@ static double local_limit_s() {
     return v;
 }
 // the limit a wait of this context has: TKHIP_WAIT_S with peers, else TKHIP_LOCAL_WAIT_S (0: none)
-static double ctx_wait_limit(const tk_ctx* c) { return c->comm ? wait_limit_s() : local_limit_s(); }
+static double ctx_wait_limit(const tk_ctx* c) { return has_peers(c) ? wait_limit_s() : local_limit_s(); }
 
 struct Deadline {
     typedef std::chrono::steady_clock clk;
@@ -262,7 +286,7 @@ static tk_status local_expired(const char* what, double lim) {
 }
 
 static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int slot = -1) {
-    if (!c->comm && local_limit_s() <= 0) {
+    if (!has_peers(c) && local_limit_s() <= 0) {
         const hipError_t e = hipStreamSynchronize(s);
         return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
     }
@@ -271,13 +295,13 @@ static tk_status sync_bounded(tk_ctx* c, hipStream_t s, const char* what, int sl
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) return TK_OK;
         if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-        if (dl.tick()) return c->comm ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
+        if (dl.tick()) return has_peers(c) ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
     }
 }
 
 // hipEventSynchronize with a deadline
 static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int slot = -1) {
-    if (!c->comm && local_limit_s() <= 0) {
+    if (!has_peers(c) && local_limit_s() <= 0) {
         const hipError_t e = hipEventSynchronize(ev);
         return e == hipSuccess ? TK_OK : fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
     }
@@ -286,8 +310,18 @@ static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int s
         const hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) return TK_OK;
         if (e != hipErrorNotReady) return fail(TK_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
-        if (dl.tick()) return c->comm ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
+        if (dl.tick()) return has_peers(c) ? wait_expired(c, what, slot) : local_expired(what, dl.lim);
     }
+}
+
+// A fused one-sweep launch's wait for its in-launch reducers gave up (the context's error
+// word, set by the device): results handed out after that are wrong.  Checked after every
+// device-completion point that hands results to the caller
+static tk_status werr_check(const tk_ctx* c, const char* what) {
+    if (c->werr && __atomic_load_n(c->werr, __ATOMIC_ACQUIRE))
+        return fail(TK_ERR_INTERNAL, "%s: a fused one-sweep launch's wait for its reducers gave up, so the "
+                                     "records of that step are wrong (TKHIP_D1_FUSE=0 avoids the fused launch)", what);
+    return TK_OK;
 }
 
 #define STUCKCHK(c)                                                                                   \
@@ -296,6 +330,230 @@ static tk_status event_bounded(tk_ctx* c, hipEvent_t ev, const char* what, int s
             return fail(TK_ERR_RCCL, "the communicator is unusable: an earlier wait on the other ranks " \
                                      "expired (TKHIP_WAIT_S)");                                       \
     } while (0)
+
+
+// ------------------------------------------------------------------ test transport
+// Several processes on ONE GPU cannot form an RCCL communicator (RCCL refuses: "Duplicate GPU
+// detected"), so the multi-rank exchange -- factor groups under an exchange, per-factor signal
+// words, alternating send buffers, coalesced slot guards, the evaluation mailbox, replicas --
+// is exercised with real peer processes through this stand-in for ncclAllReduce (test build
+// only).  Node-local POSIX shared memory /dev/shm/tkhip_tc_<key> holds, per rank, two buffers
+// (by collective sequence parity), a posted word per buffer and a consumed word.  Collective
+// number s: wait until every rank has consumed s-2 (the buffer's last use), copy this rank's
+// contribution in, post s, wait for every rank's post of s, combine in rank order (sum or
+// max: the records exchange adds zeros to each row, so the sum is exact), consume s.  The
+// records exchange stays stream-ordered on the exchange stream: send rows -> pinned host
+// (hipMemcpyAsync), the combine in a host function (hipLaunchHostFunc), result -> the receive
+// buffer; every rank issues the same collectives in the same order (tk_xsched.h), so the
+// sequence numbers agree.  Host all-reduces (preflight, agreements) wait for the exchange
+// stream first and combine on the host directly.  Every wait is bounded by TKHIP_WAIT_S.
+#if TK_TEST_BUILD
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+struct TcRank {
+    std::atomic<unsigned long long> posted[2];
+    std::atomic<unsigned long long> consumed;
+    char pad[40];
+};
+struct TcHdr {
+    std::atomic<unsigned long long> attached;
+    unsigned long long nranks, cap, magic;
+    char pad[32];
+};
+static_assert(sizeof(TcRank) == 64 && sizeof(TcHdr) == 64, "shared-memory layout");
+struct TestComm {
+    TcHdr* hdr = nullptr;
+    size_t bytes = 0;
+    int nranks = 1, rank = 0;
+    size_t cap = 0;                     // doubles per buffer
+    unsigned long long seq = 0;         // collectives issued by this process
+    double* hsend = nullptr;            // pinned staging of the records exchange
+    double* hrecv = nullptr;
+    size_t hcap = 0;
+    std::atomic<int> failed{0};         // a wait expired inside a host function
+    TcRank* rk(int q) const {
+        return (TcRank*)((char*)hdr + sizeof(TcHdr) + (size_t)q * (sizeof(TcRank) + 2 * cap * sizeof(double)));
+    }
+    double* buf(int q, int p) const { return (double*)(rk(q) + 1) + (size_t)p * cap; }
+};
+static const unsigned long long TC_MAGIC = 0x746b68697074636dull;
+
+// one chunk (n <= cap) of collective number s; false when a wait expired (out is NaN then)
+static bool tc_chunk(TestComm* tc, const double* in, double* out, size_t n, bool mx, unsigned long long s) {
+    const int p = (int)(s & 1);
+    Deadline dl(wait_limit_s());
+    auto wait_all = [&](auto pred) {
+        for (int q = 0; q < tc->nranks; ++q)
+            while (!pred(tc->rk(q)))
+                if (dl.tick()) return false;
+        return true;
+    };
+    bool ok = s <= 2 || wait_all([&](TcRank* r) { return r->consumed.load(std::memory_order_acquire) >= s - 2; });
+    TcRank* me = tc->rk(tc->rank);
+    if (ok) {
+        memcpy(tc->buf(tc->rank, p), in, n * sizeof(double));
+        me->posted[p].store(s, std::memory_order_release);
+        ok = wait_all([&](TcRank* r) { return r->posted[p].load(std::memory_order_acquire) >= s; });
+    }
+    if (!ok) {
+        for (size_t i = 0; i < n; ++i) out[i] = NAN;
+        tc->failed.store(1);
+        return false;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        double a = tc->buf(0, p)[i];
+        for (int q = 1; q < tc->nranks; ++q) {
+            const double b = tc->buf(q, p)[i];
+            a = mx ? (b > a ? b : a) : a + b;
+        }
+        out[i] = a;
+    }
+    me->consumed.store(s, std::memory_order_release);
+    return true;
+}
+// a collective over any count: ceil(count / cap) sequence numbers from seq0
+static bool tc_run(TestComm* tc, const double* in, double* out, size_t count, bool mx, unsigned long long seq0) {
+    bool ok = true;
+    for (size_t off = 0, k = 0; off < count || (count == 0 && k == 0); off += tc->cap, ++k) {
+        const size_t n = std::min(tc->cap, count - off);
+        ok = tc_chunk(tc, in + off, out + off, n, mx, seq0 + k) && ok;
+        if (count == 0) break;
+    }
+    return ok;
+}
+static unsigned long long tc_nseq(const TestComm* tc, size_t count) {
+    return count == 0 ? 1 : (count + tc->cap - 1) / tc->cap;
+}
+static tk_status tc_allreduce(tk_ctx* c, const double* in, double* out, size_t count, bool mx, const char* what) {
+    TestComm* tc = c->tcomm;
+    const unsigned long long s0 = tc->seq + 1;
+    tc->seq += tc_nseq(tc, count);
+    if (tc->failed.load() || !tc_run(tc, in, out, count, mx, s0)) return wait_expired(c, what, -1);
+    return TK_OK;
+}
+struct TcJob {
+    TestComm* tc;
+    size_t n;
+    unsigned long long s0;
+};
+static void tc_job_cb(void* arg) {
+    TcJob* jb = (TcJob*)arg;
+    if (!jb->tc->failed.load()) tc_run(jb->tc, jb->tc->hsend, jb->tc->hrecv, jb->n, false, jb->s0);
+    delete jb;
+}
+static tk_status tc_exchange(tk_ctx* c, const double* s, double* r, size_t tot, hipStream_t st) {
+    TestComm* tc = c->tcomm;
+    if (tc->failed.load()) return wait_expired(c, "records exchange (test transport)", -1);
+    if (tot > tc->hcap) {
+        tk_status sb = sync_bounded(c, st, "test transport staging");
+        if (sb) return sb;
+        if (tc->hsend) hipHostFree(tc->hsend);
+        if (tc->hrecv) hipHostFree(tc->hrecv);
+        tc->hsend = tc->hrecv = nullptr;
+        tc->hcap = 0;
+        HIPCHK(hipHostMalloc((void**)&tc->hsend, tot * sizeof(double), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&tc->hrecv, tot * sizeof(double), hipHostMallocDefault));
+        tc->hcap = tot;
+    }
+    TcJob* jb = new TcJob{tc, tot, tc->seq + 1};
+    tc->seq += tc_nseq(tc, tot);
+    HIPCHK(hipMemcpyAsync(tc->hsend, s, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    hipError_t e = hipLaunchHostFunc(st, tc_job_cb, jb);
+    if (e != hipSuccess) {
+        delete jb;
+        return fail(TK_ERR_HIP, "hipLaunchHostFunc: %s", hipGetErrorString(e));
+    }
+    HIPCHK(hipMemcpyAsync(r, tc->hrecv, tot * sizeof(double), hipMemcpyHostToDevice, st));
+    return TK_OK;
+}
+static void tc_destroy(tk_ctx* c) {
+    TestComm* tc = c->tcomm;
+    if (!tc) return;
+    if (tc->hsend) hipHostFree(tc->hsend);
+    if (tc->hrecv) hipHostFree(tc->hrecv);
+    if (tc->hdr) munmap(tc->hdr, tc->bytes);
+    delete tc;
+    c->tcomm = nullptr;
+}
+extern "C" tk_status tk_comm_init_test(tk_ctx* c, const char* key, int nranks, int rank) { TK_API_BEGIN
+    CHECKARG(c && key && nranks >= 1 && rank >= 0 && rank < nranks, "bad argument");
+    CHECKARG(!c->comm && !c->tcomm, "the context already has a communicator");
+    for (const char* q = key; *q; ++q)
+        CHECKARG((*q >= '0' && *q <= '9') || (*q >= 'a' && *q <= 'z') || (*q >= 'A' && *q <= 'Z') || *q == '_',
+                 "key must be [0-9A-Za-z_]");
+    char name[200];
+    snprintf(name, sizeof name, "/dev/shm/tkhip_tc_%s", key);
+    const size_t cap = 1 << 16;
+    const size_t bytes = sizeof(TcHdr) + (size_t)nranks * (sizeof(TcRank) + 2 * cap * sizeof(double));
+    Deadline dl(wait_limit_s());
+    TcHdr* h = nullptr;
+    if (rank == 0) {
+        char tmp[220];
+        snprintf(tmp, sizeof tmp, "%s.%d.tmp", name, (int)getpid());
+        int fd = open(tmp, O_RDWR | O_CREAT | O_EXCL, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) {
+            if (fd >= 0) close(fd), unlink(tmp);
+            return fail(TK_ERR_STATE, "tk_comm_init_test: cannot create %s", tmp);
+        }
+        void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m == MAP_FAILED) {
+            unlink(tmp);
+            return fail(TK_ERR_STATE, "tk_comm_init_test: mmap failed");
+        }
+        memset(m, 0, bytes);
+        h = (TcHdr*)m;
+        h->nranks = (unsigned long long)nranks;
+        h->cap = cap;
+        h->magic = TC_MAGIC;
+        h->attached.store(1, std::memory_order_release);
+        if (rename(tmp, name) != 0) {
+            munmap(m, bytes);
+            unlink(tmp);
+            return fail(TK_ERR_STATE, "tk_comm_init_test: cannot publish %s", name);
+        }
+        while (h->attached.load(std::memory_order_acquire) < (unsigned long long)nranks)
+            if (dl.tick()) {
+                unlink(name);
+                munmap(m, bytes);
+                return fail(TK_ERR_RCCL, "tk_comm_init_test: only %llu of %d ranks attached", h->attached.load(), nranks);
+            }
+        unlink(name);   // every rank holds its mapping: nothing is left in /dev/shm
+    } else {
+        int fd;
+        while ((fd = open(name, O_RDWR)) < 0)
+            if (dl.tick()) return fail(TK_ERR_RCCL, "tk_comm_init_test: rank 0 never published %s", name);
+        struct stat sb;
+        void* m = (fstat(fd, &sb) == 0 && (size_t)sb.st_size == bytes)
+                      ? mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+        close(fd);
+        h = (TcHdr*)m;
+        if (m == MAP_FAILED || h->magic != TC_MAGIC || h->nranks != (unsigned long long)nranks || h->cap != cap) {
+            if (m != MAP_FAILED) munmap(m, bytes);
+            return fail(TK_ERR_STATE, "tk_comm_init_test: %s does not describe this job", name);
+        }
+        h->attached.fetch_add(1, std::memory_order_acq_rel);
+    }
+    TestComm* tc = new TestComm();
+    tc->hdr = h;
+    tc->bytes = bytes;
+    tc->nranks = nranks;
+    tc->rank = rank;
+    tc->cap = cap;
+    c->tcomm = tc;
+    c->nranks = nranks;
+    c->rank = rank;
+    return TK_OK;
+    TK_API_END
+}
+#else
+struct TestComm {};
+static tk_status tc_allreduce(tk_ctx*, const double*, double*, size_t, bool, const char*) { return TK_ERR_INTERNAL; }
+static tk_status tc_exchange(tk_ctx*, const double*, double*, size_t, hipStream_t) { return TK_ERR_INTERNAL; }
+static void tc_destroy(tk_ctx*) {}
+#endif
 
 extern "C" {
 
@@ -322,6 +580,19 @@ tk_status tk_ctx_create(int device, tk_ctx** out) { TK_API_BEGIN
         delete c;
         return fail(TK_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    {
+        void* hp = nullptr;
+        if (hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+            hipStreamDestroy(c->stream);
+            hipStreamDestroy(c->xstream);
+            hipStreamDestroy(c->gstream);
+            hipStreamDestroy(c->fstream);
+            delete c;
+            return fail(TK_ERR_ALLOC, "tk_ctx_create: error word");
+        }
+        c->werr = (unsigned int*)hp;
+        *c->werr = 0;
+    }
     *out = c;
     return TK_OK;
     TK_API_END
@@ -339,7 +610,9 @@ static void ctx_release(tk_ctx* c) {
     drain_timers(c);
     for (hipEvent_t e : c->evpool) hipEventDestroy(e);
     if (c->comm) ncclCommDestroy(c->comm);
+    tc_destroy(c);
     if (c->xbuf) hipFree(c->xbuf);
+    if (c->werr) hipHostFree(c->werr);
     hipStreamDestroy(c->stream);
     hipStreamDestroy(c->xstream);
     hipStreamDestroy(c->gstream);
@@ -361,7 +634,8 @@ tk_status tk_ctx_sync(tk_ctx* c) { TK_API_BEGIN
     tk_status st = sync_bounded(c, c->stream, "tk_ctx_sync (compute stream)");
     if (st == TK_OK) st = sync_bounded(c, c->gstream, "tk_ctx_sync (Gram stream)");
     if (st == TK_OK) st = sync_bounded(c, c->fstream, "tk_ctx_sync (factor-group stream)");
-    return st ? st : sync_bounded(c, c->xstream, "tk_ctx_sync (exchange stream)");
+    if (st == TK_OK) st = sync_bounded(c, c->xstream, "tk_ctx_sync (exchange stream)");
+    return st ? st : werr_check(c, "tk_ctx_sync");
     TK_API_END
 }
 
@@ -401,6 +675,7 @@ static tk_status host_allreduce(tk_ctx* c, double* buf, size_t count, ncclRedOp_
     }
     tk_status st = sync_bounded(c, c->xstream, what);
     if (st) return st;
+    if (c->tcomm) return tc_allreduce(c, buf, buf, count, op == ncclMax, what);   // (host memory already)
     HIPCHK(hipMemcpyAsync(c->xbuf, buf, count * sizeof(double), hipMemcpyHostToDevice, c->stream));
     NCCLCHK(ncclAllReduce(c->xbuf, c->xbuf, count, ncclDouble, op, c->comm, c->stream));
     HIPCHK(hipMemcpyAsync(buf, c->xbuf, count * sizeof(double), hipMemcpyDeviceToHost, c->stream));
@@ -409,7 +684,7 @@ static tk_status host_allreduce(tk_ctx* c, double* buf, size_t count, ncclRedOp_
 
 tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_BEGIN
     CHECKARG(c && buf, "NULL argument");
-    if (!c->comm || c->nranks == 1) return TK_OK;
+    if (!has_peers(c) || c->nranks == 1) return TK_OK;
     return host_allreduce(c, buf, count, ncclSum, "tk_comm_allreduce_host");
     TK_API_END
 }
@@ -417,6 +692,7 @@ tk_status tk_comm_allreduce_host(tk_ctx* c, double* buf, size_t count) { TK_API_
 tk_status tk_comm_count(tk_ctx* c, int* nranks_out) { TK_API_BEGIN
     CHECKARG(c && nranks_out, "NULL argument");
     *nranks_out = 0;
+    if (c->tcomm) *nranks_out = c->nranks;
     if (!c->comm) return TK_OK;
     int n = 0;
     NCCLCHK(ncclCommCount(c->comm, &n));
@@ -894,7 +1170,6 @@ static void free_decomp(tk_decomp* dc) {
     if (dc->gram_scr && !dc->gram_scr_owned_by_allocs) hipFree(dc->gram_scr);
     if (dc->gram_host) hipHostFree(dc->gram_host);
     if (dc->gram_done) hipHostFree(dc->gram_done);
-    if (dc->werr) hipHostFree(dc->werr);
     if (dc->xflag) hipFree(dc->xflag);
     for (unsigned long long* p : dc->xsig) hipFree(p);
     if (dc->stallw) hipFree(dc->stallw);
@@ -1202,15 +1477,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         if (e != hipSuccess) { free_decomp(dc); return fail(TK_ERR_HIP, "upload descriptors: %s", hipGetErrorString(e)); }
     }
     DA(dc->rec, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
-    if (dc->fuse) {
-        void* hp = nullptr;
-        if (hipHostMalloc(&hp, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-            free_decomp(dc);
-            return fail(TK_ERR_ALLOC, "tk_decomp_create: fused-launch error word");
-        }
-        dc->werr = (unsigned int*)hp;
-        *dc->werr = 0;
-    }
+    if (dc->fuse) dc->werr = c->werr;   // (the context's: not owned here)
     // the deferred Gram's partials (tk_decomp_gram), allocated with the rest: an allocation at
     // the first call cost up to ~15 ms inside the driver loop
     if (dc->gram_deferred && nf > 0) {
@@ -1237,13 +1504,13 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     }
     // records go through the RCCL exchange whenever factors are spread over ranks;
     // TKHIP_EXCHANGE_ALWAYS=1 takes that path on a 1-rank communicator too (tests, bench)
-    if (const char* ef = getenv("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
+    if (const char* ef = TEST_ENV("TKHIP_TEST_FAIL_STEP")) dc->fail_step = atoi(ef);
     if (const char* eg = getenv("TKHIP_TEST_GROUP_DELAY_US")) dc->gdelay_us = std::max(0.0, atof(eg));
-    if (const char* ek = getenv("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
+    if (const char* ek = TEST_ENV("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
     if (const char* eb = getenv("TKHIP_BK_FOLD")) dc->bk_fold = eb[0] != '0';
     dc->bk_fold = dc->bk_fold && TK_D1_ONEWIN;   // (the window-loop kernel has no bookkeeping blocks)
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
-    if (c->comm && (c->nranks > 1 || (xa && xa[0] == '1'))) {
+    if (has_peers(c) && (c->nranks > 1 || (xa && xa[0] == '1'))) {
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
         DA(dc->rec_alt, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));
     } else
@@ -1289,7 +1556,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         // bookkeeping block stores the step's KArgs::xval there -- a posted store where an add was
         // a round trip the launch waited for -- and the exchange waits for every word
         // (exchange_range).  Allocation failure: the one shared word with adds
-        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");
+        const char* esh = TEST_ENV("TKHIP_TEST_SHARED_XSIG");
         bool okw = !(esh && esh[0] == '1');
         for (int f = 0; okw && f < nf; ++f) {
             void* p = nullptr;
@@ -1336,7 +1603,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
             ok = hipEventCreateWithFlags(&dc->fev_join[g], hipEventDisableTiming | hipEventDisableSystemFence) == hipSuccess;
         // (factor groups under an exchange need the per-factor words; TKHIP_TEST_SHARED_XSIG=1,
         // diagnostics only, runs them on the round-4 shared count)
-        const char* esh = getenv("TKHIP_TEST_SHARED_XSIG");
+        const char* esh = TEST_ENV("TKHIP_TEST_SHARED_XSIG");
         ok = ok && (dc->recv == dc->rec || !dc->xsig.empty() || (esh && esh[0] == '1'));
         if (ok) {
             dc->ngr = G;
@@ -1385,7 +1652,7 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         dc->xslot_seq_alt = dc->xslot_seq;
         dc->xev_alt = dc->xev;
         if (const char* eg = getenv("TKHIP_XCH_GROUP")) dc->xs.group = std::min(64, std::max(1, atoi(eg)));
-        if (const char* es = getenv("TKHIP_TEST_XCH_STALL")) {
+        if (const char* es = TEST_ENV("TKHIP_TEST_XCH_STALL")) {
             void* p = nullptr;
             if (dc->recv != dc->rec && hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory) == hipSuccess && p) {
                 if (hipMemcpy(&dc->stall_v, p, 8, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -1492,10 +1759,12 @@ tk_status tk_decomp_destroy(tk_decomp* dc) { TK_API_BEGIN
     if (!c->stuck) sync_bounded(c, c->xstream, "tk_decomp_destroy (exchange stream)");
     if (!c->stuck) sync_bounded(c, c->gstream, "tk_decomp_destroy (Gram stream)");
     if (!c->stuck) sync_bounded(c, c->fstream, "tk_decomp_destroy (factor-group stream)");
+    // (the handle is released either way; a fused wait that gave up is still reported)
+    const tk_status sw = dc->werr ? werr_check(c, "tk_decomp_destroy") : TK_OK;
     free_decomp(dc);
     for (tk_mat* A : mats) mat_release(A);
     ctx_release(c);
-    return TK_OK;
+    return sw;
     TK_API_END
 }
 
@@ -1511,7 +1780,7 @@ static tk_status slot_guard(tk_decomp* dc, int slot) {
     HpScope hp_(HP_GUARD);
     if (dc->recv == dc->rec) return TK_OK;
     static const bool noguard = [] {   // (TKHIP_TEST_NO_GUARD=1: timing only, records may be torn)
-        const char* e = getenv("TKHIP_TEST_NO_GUARD");
+        const char* e = TEST_ENV("TKHIP_TEST_NO_GUARD");
         return e && e[0] == '1';
     }();
     if (noguard) return TK_OK;
@@ -1568,6 +1837,20 @@ static tk_status join_groups(tk_decomp* dc) {
         if (gj_) return gj_;                   \
     } while (0)
 
+// polls of a fused launch's bounded wait before it gives up (fuse_wait): 2^22 (~0.2 s of
+// s_sleep); a test build lowers it with TKHIP_TEST_FUSE_SPIN to make the wait expire
+static unsigned fuse_spin() {
+#if TK_TEST_BUILD
+    static const unsigned v = [] {
+        const char* e = getenv("TKHIP_TEST_FUSE_SPIN");
+        return e ? (unsigned)atol(e) : (1u << 22);
+    }();
+    return v;
+#else
+    return 1u << 22;
+#endif
+}
+
 static KArgs base_args(tk_decomp* dc, int j, int slot) {
     KArgs a;
     a.n = dc->n;
@@ -1592,6 +1875,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.redmm = 0;
     a.wseq = 0;
     a.werr = nullptr;
+    a.wspin = fuse_spin();
     a.wsc = 0;
     a.xval = 0;
     return a;
@@ -1643,17 +1927,22 @@ static tk_status exchange_range(tk_decomp* dc, int s0, int s1) {
         }
         // TKHIP_TEST_XCH_SKIP (timing only, wrong records): 1 no mirror kernel, 2 no all-reduce
         static const int xskip = [] {
-            const char* e = getenv("TKHIP_TEST_XCH_SKIP");
+            const char* e = TEST_ENV("TKHIP_TEST_XCH_SKIP");
             return e ? atoi(e) : 0;
         }();
         HpScope hp_n(HP_NCCL);
-        if (!(xskip & 2)) NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
+        if (c->tcomm) {
+            tk_status sx = tc_exchange(c, s, r, tot, c->xstream);
+            if (sx) return sx;
+        } else if (!(xskip & 2)) {
+            NCCLCHK(ncclAllReduce(s, r, tot, ncclDouble, ncclSum, c->comm, c->xstream));
+        }
     }
     HIPCHK(hipEventRecord(dc->ev_x[s1], c->xstream));
     ++dc->ev_x_gen[s1];
     for (int sl = s0; sl <= s1; ++sl) dc->xev[sl] = s1;
     static const bool nomirror = [] {
-        const char* e = getenv("TKHIP_TEST_XCH_SKIP");
+        const char* e = TEST_ENV("TKHIP_TEST_XCH_SKIP");
         return e && (atoi(e) & 1);
     }();
     if (dc->xdone && !nomirror) {
@@ -1732,8 +2021,10 @@ static void complete_step(tk_decomp* dc, int j, unsigned long long seqj, unsigne
 // k_reduce256 of its own (its last block also evaluates the next step's scalars).  Local only.
 static tk_status red_flush(tk_decomp* dc) {
     if (dc->red_j < 0) return TK_OK;
-    if (dc->werr && __atomic_load_n(dc->werr, __ATOMIC_ACQUIRE))
-        return fail(TK_ERR_INTERNAL, "a fused one-sweep launch's wait for its reducers gave up (TKHIP_D1_FUSE=0 avoids it)");
+    if (dc->werr) {
+        tk_status sw = werr_check(dc->ctx, "red_flush");
+        if (sw) return sw;
+    }
     GJOIN(dc);
     const int j = dc->red_j;
     dc->red_j = -1;
@@ -2123,8 +2414,12 @@ tk_status tk_decomp_step(tk_decomp* dc, int j, double* rec_out) { TK_API_BEGIN
     HpScope hp_step(HP_STEP);
     const int prev_bk = dc->bk_j;
     const unsigned long long prev_seq = dc->bk_args.seq, prev_xval = dc->bk_args.xval;
+#if TK_TEST_BUILD
     tk_status st = j == dc->fail_step ? fail(TK_ERR_HIP, "step %d: injected failure (TKHIP_TEST_FAIL_STEP)", j)
                                       : step_impl(dc, j, rec_out);
+#else
+    tk_status st = step_impl(dc, j, rec_out);
+#endif
     if (st) {
         // the exchange stream only ever waits for signal counts of steps that were fully
         // enqueued, so a failed step cannot leave it blocked (destroy stays safe)
@@ -2263,7 +2558,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
             }
         }
         memcpy(out, dc->hrec + (size_t)s0 * per, (s1 - s0) * per * sizeof(double));
-        return TK_OK;
+        return werr_check(c, "tk_decomp_records");
     }
     bool xhosted = dc->xdone != nullptr;
     for (int sl = s0; sl < s1 && xhosted; ++sl) xhosted = dc->xslot_seq[sl] != 0;
@@ -2290,7 +2585,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
             }
         }
         memcpy(out, dc->hrec + (size_t)s0 * per, (s1 - s0) * per * sizeof(double));
-        return TK_OK;
+        return werr_check(c, "tk_decomp_records");
     }
     if (dc->cstream && dc->recv != dc->rec) {
         // multi-rank: the slots are final once the exchange of the last one has run
@@ -2303,7 +2598,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
         HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                               dc->cstream));
         HIPCHK(hipStreamSynchronize(dc->cstream));
-        return TK_OK;
+        return werr_check(c, "tk_decomp_records");
     }
     if (dc->recv != dc->rec) {
         tk_status st = sync_bounded(c, c->xstream, "records exchange", s1 - 1);
@@ -2313,7 +2608,7 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
     HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                           c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    return TK_OK;
+    return werr_check(c, "tk_decomp_records");
     TK_API_END
 }
 
@@ -2351,7 +2646,7 @@ tk_status tk_decomp_get_basis(tk_decomp* dc, int f, int c0, int nc, double* out)
         HIPCHK(hipMemcpy(out + (size_t)cc * dc->n, dc->scratch, (size_t)dc->n * m * sizeof(double),
                          hipMemcpyDeviceToHost));
     }
-    return TK_OK;
+    return werr_check(dc->ctx, "tk_decomp_get_basis");
     TK_API_END
 }
 
@@ -2371,7 +2666,7 @@ static tk_status gram_wait(tk_decomp* dc, hipStream_t s, unsigned long long want
                 return fail(TK_ERR_HIP, "tk_decomp_gram: not complete after %.0f s", dl.lim);
         }
     }
-    return TK_OK;
+    return werr_check(c, "tk_decomp_gram");
 }
 
 tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
@@ -2447,6 +2742,8 @@ tk_status tk_decomp_gram(tk_decomp* dc, int f, int k, double* G) { TK_API_BEGIN
         vbuf.resize(nv);
         HIPCHK(hipMemcpyAsync(vbuf.data(), res, nv * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        tk_status sw = werr_check(c, "tk_decomp_gram");
+        if (sw) return sw;
         v = vbuf.data();
     }
     gram_unpack(k, v, G);
@@ -2589,6 +2886,7 @@ tk_status tk_decomp_basis_mul(tk_decomp* dc, int k, int t, const double* Y, doub
                 for (int64_t r = 0; r < dc->n; ++r)
                     Xf[(size_t)q * dc->n + r] = tmp[(size_t)(r >> 8) * 256 * t + (size_t)q * 256 + (r & 255)];
         }
+        return werr_check(c, "tk_decomp_basis_mul");
     }
     return TK_OK;
     TK_API_END

@@ -119,7 +119,8 @@ struct KArgs {
     int red;          // fused one-sweep launch: its leading blocks reduce step j-1's partials
     int redmm;        // ... with the memory-model hand-off (red_mm())
     unsigned long long wseq;   // ... and publish this in each factor's step word (DFac::rword)
-    unsigned int* werr;        // ... a wait that gave up sets this (host-mapped)
+    unsigned int* werr;        // ... a wait that gave up sets this (host-mapped, the context's)
+    unsigned int wspin;        // ... polls before a wait gives up (2^22; a test build may lower it)
     // one-sweep Arnoldi, one stream (no factor groups): the step's reduce is a plain reduction and
     // the windows evaluate the next step's scalars (d1_scalars); 0: the reduce's last block does
     // and stores them (with two group streams that reduce hides behind the other group's sweep)

@@ -448,13 +448,20 @@ __device__ __forceinline__ double ld_ag(const double* p) {
 }
 // Fused one-sweep launch: one lane polls the factor's step word (sc1 loads, s_sleep between)
 // until the in-launch reducers publish `want`; the block's waves pass a barrier after it.
-// Bounded: after ~2^22 polls the error word is set (the host reports TK_ERR_INTERNAL) and the
-// block goes on -- a result would be wrong, but nothing hangs.
-__device__ __forceinline__ void fuse_wait(const unsigned long long* word, unsigned long long want, unsigned int* err) {
+// Bounded: after `spin` polls (2^22) the context's error word is set -- every host call that
+// hands results out after a sync then returns TK_ERR_INTERNAL -- and the block goes on: a
+// result would be wrong, but nothing hangs.
+// mm (the memory-model hand-off, red_mm()): the reducers' last block stores the word with
+// release; every wave then takes an agent-scope acquire fence after the barrier, so the
+// values it loads next are ordered after the word (a relaxed poll that reads a release store,
+// then an acquire fence, synchronizes with it).  Without mm the measured relaxed form: sc1
+// stores drained before the word, sc1 loads after it.
+__device__ __forceinline__ void fuse_wait(const unsigned long long* word, unsigned long long want, unsigned int* err,
+                                          unsigned spin, int mm) {
     if (threadIdx.x == 0) {
         unsigned spins = 0;
         while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
-            if (++spins > (1u << 22)) {
+            if (++spins > spin) {
                 if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 break;
             }
@@ -462,43 +469,7 @@ __device__ __forceinline__ void fuse_wait(const unsigned long long* word, unsign
         }
     }
     __syncthreads();
-}
-// Same, with columns c < LC read from LDS (pair p of this thread's row at vl[p * TPB + t], zero
-// for rows outside the basis) as each chunk of 8 is reached: the same order, so bitwise equal.
-template <int MAXC, int LC>
-__device__ __forceinline__ void row_dot2_lc(const Row<MAXC>& R, const d2_t* vl, int t, bool inb,
-                                            const double* __restrict__ h, const double* __restrict__ g,
-                                            double& sh, double& sg) {
-    double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-    uint64_t ph = (uint64_t)h, pg = (uint64_t)g;
-#pragma unroll
-    for (int c0 = 0; c0 < MAXC; c0 += 8) {
-        __builtin_amdgcn_sched_barrier(0);
-        asm volatile("" : "+s"(ph), "+s"(pg) : "v"(a0), "v"(b0));
-        const double* hh = (const double*)ph;
-        const double* gg = (const double*)pg;
-        double cv[8];
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-            if (c0 + i < LC) {
-                const d2_t x = vl[((c0 + i) >> 1) * TPB + t];
-                cv[i] = inb ? x.x : 0.0;
-                cv[i + 1] = inb ? x.y : 0.0;
-            } else {
-                cv[i] = R.v[c0 + i < MAXC ? c0 + i : 0];
-                cv[i + 1] = R.v[c0 + i + 1 < MAXC ? c0 + i + 1 : 0];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i += 2) {
-            a0 += cv[i] * CP4(hh)[c0 + i];
-            a1 += cv[i + 1] * CP4(hh)[c0 + i + 1];
-            b0 += cv[i] * CP4(gg)[c0 + i];
-            b1 += cv[i + 1] * CP4(gg)[c0 + i + 1];
-        }
-    }
-    sh = a0 + a1;
-    sg = b0 + b1;
+    if (mm) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 // Same with both coefficient vectors staged in LDS (broadcast ds_read_b128), same order;
 // coefficient reads in groups of GRP columns (register pressure).
@@ -972,12 +943,6 @@ __global__ __launch_bounds__(TPB) OCC_ATTR(32, 48) void k_arn_finalize(const DFa
 __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= TPB ? TPB - 1 : (int)i); }
 
 
-#ifndef TK_BK_TEST
-#define TK_BK_TEST 0
-#endif
-#ifndef TK_VY_TEST
-#define TK_VY_TEST 0
-#endif
 // fused flush + V*Y (k_fin_vy): 4 waves per SIMD up to this register-row width (56 spills to
 // scratch at 4), Y coefficient reads from LDS in groups of this many columns
 #ifndef TK_VY_OCC4
@@ -994,10 +959,6 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_L3
 #define TK_D1_L3 56
 #endif
-// coefficients through the scalar cache (0) or staged in LDS (1: measured slower, VGPR spills)
-#ifndef TK_D1_COEF_LDS
-#define TK_D1_COEF_LDS 0
-#endif
 // Column dots: per window each 16-lane row of a wave reduce-scatters its products (rs16)
 // and every lane adds its result into a private LDS slot -- no barrier; the slots are
 // combined once, after the last window.  Chunk k < NUZ holds columns 8k..8k+7 times
@@ -1008,23 +969,6 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_RS64
 #define TK_D1_RS64 1
 #endif
-#ifndef TK_D1_XMAP
-#define TK_D1_XMAP 0
-#endif
-// Register rows of at least TK_D1_LCMIN columns keep their lowest TK_D1_LC columns in LDS,
-// loaded there directly (buffer_load ... lds, no VGPR destination) and read back as each use
-// comes: the register budget of a row TK_D1_LC columns narrower -- one wave per SIMD more,
-// so more rows' loads in flight per CU -- for 32 KB of LDS per block (0 = all in registers)
-#ifndef TK_D1_LC
-#define TK_D1_LC 0   // measured 2.6 % slower at 16 (profiles/r03/d1_ldscols_ab.txt): off
-#endif
-#ifndef TK_D1_LCMIN
-#define TK_D1_LCMIN 48
-#endif
-#ifndef TK_D1_LCMAX
-#define TK_D1_LCMAX 48   // (56 columns with 16 in LDS still spill 22 registers at 4 waves)
-#endif
-#define D1_LCOLS(M) (TK_D1_LC > 0 && TK_D1_RS64 && TK_D1_SWPIN && (M) >= TK_D1_LCMIN && (M) <= TK_D1_LCMAX ? TK_D1_LC : 0)
 #ifndef TK_D1_SWPIN
 #define TK_D1_SWPIN 1
 #endif
@@ -1077,9 +1021,7 @@ template <int MAXC, int FMT, int MODE>
 #if TK_D1_OCCT
 // narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
 #if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
-// (with TK_D1_LC the top tiers keep their low TK_D1_LC columns in LDS: the register row is
-// TK_D1_LC columns narrower, and so is the tier)
-#define D1_RC (MAXC - D1_LCOLS(MAXC))
+#define D1_RC MAXC
 #define D1_OCC (D1_RC <= 8 ? 8 : (D1_RC <= 16 ? 6 : (D1_RC <= 24 ? 5 : (D1_RC <= TK_D1_L4 ? 4 : (D1_RC <= TK_D1_L3 ? 3 : 2)))))
 #else
 #define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
@@ -1090,7 +1032,6 @@ template <int MAXC, int FMT, int MODE>
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a,
                                                                                                   KArgs b) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
-    constexpr int LC = D1_LCOLS(MAXC);   // low columns of the row kept in LDS (TK_D1_LC)
     // MODE bit 0 (VC): the basis rows through the caches (the launcher's choice while the rank's
     // per-step working set fits the Infinity Cache), else nt.  Bit 1 (FUSE): the previous step's
     // reduce runs in this launch's leading blocks (a.red) -- the window blocks issue their row
@@ -1100,13 +1041,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // Bit 2 (WSC, one stream only): the previous step's reduce was a plain reduction -- wave 0
     // evaluates the step's scalars (d1_scalars) and hands them to the block through LDS
     constexpr bool WSC = (MODE & 4) != 0 && !FUSE;
-    static_assert(!FUSE || LC == 0, "fused launches keep the whole register row in VGPRs");
-    static_assert(LC % 8 == 0 && (LC == 0 || LC <= MAXC - 8), "LDS columns: whole chunks of 8, below the patched pairs");
     __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
     __shared__ double d1s[WSC ? 2 : 1];                // the step's ib, gamma (wave 0 -> the block)
-#if TK_D1_COEF_LDS
-    __shared__ __attribute__((aligned(16))) double cl[2][MAXC];   // c, h1
-#endif
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const DFac& d = F[blockIdx.y];
 #if TK_D1_ONEWIN
@@ -1135,19 +1071,18 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     }
     const int x0 = XR + (b.j >= 0 ? 8 : 0);
     if ((int)blockIdx.x < x0) {
-        if (blockIdx.y == 0 && !(TK_BK_TEST & 2))   // (TK_BK_TEST: timing experiments)
+        if (blockIdx.y == 0)
             for (int f = (int)blockIdx.x - XR; f < (int)gridDim.y; f += 8) {
                 const DFac& df = F[f];
-                if (FUSE && a.red) fuse_wait(df.rword, a.wseq, a.werr);
+                if (FUSE && a.red) fuse_wait(df.rword, a.wseq, a.werr, a.wspin, a.redmm);
                 bk_arn_d(df, b, b.rec + (int64_t)df.gidx * b.m, lds);
-                if (!(TK_BK_TEST & 1)) post_signal(b, df, f, true, true);
+                post_signal(b, df, f, true, true);
                 __syncthreads();
             }
         return;
     }
     const int bx = (int)blockIdx.x - x0;
-    // (TK_D1_XMAP=1, A/B builds only: windows interleaved over the XCDs instead)
-    const int slot = TK_D1_XMAP ? bx : (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
+    const int slot = (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
     if (slot >= d.nwin) return;
 #else
     if ((int)blockIdx.x >= d.npd) return;
@@ -1157,35 +1092,20 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
     const int64_t TS = (int64_t)TPB * kcp(a.kmax);
-    // dynamic LDS: [ LDS columns: LC/2 pairs x TPB rows | column-dot slots ]
-    const d2_t* vl = (const d2_t*)lds;
-    double* acc = lds + LC * TPB;
+    // dynamic LDS: the column-dot slots
+    double* acc = lds;
     const int j = a.j, t = threadIdx.x;
     const int hl = d.hl, hu = d.hu, WS = TPB - 2 * (hl + hu);
     const double* Uin = a.ubuf ? d.W : d.U;
     double* Uout = a.ubuf ? d.U : d.W;
     // coefficients from the previous step's reduced dots (no post kernel in between):
     // c = RED1[0, j), q = RED1[j, 2j), scalars after them (k_reduce256)
-#if TK_BK_TEST & 16
-    const double* c = d.h2;
-    const double* qv = d.g;
-#else
     const double* c = d.RED1;
     const double* qv = d.RED1 + j;
-#endif
     const rsrc_t tv = mkrsrc(d.V, (uint32_t)(a.ntiles * TS * 8));
     const bool gram = d.track_gram != 0;
     const int nch = NUZ + 1 + (gram ? NG : 0);
     for (int e = t; e < nch * D1_CHW; e += TPB) acc[e] = 0.0;   // private slots
-#if TK_D1_COEF_LDS
-    // coefficient entries past the live ones are zero (init) and meet zero or finite
-    // basis entries
-    if (t < MAXC) {
-        cl[0][t] = ld(c, t);
-        cl[1][t] = ld(qv, t);
-    }
-    __syncthreads();
-#endif
     int par = 0;
 #if TK_D1_ONEWIN
     // one window per block (no window loop: nothing loop-invariant to hoist)
@@ -1205,15 +1125,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // column j-1 from E
         int jl = j & ~1;   // the per-pair conditions are re-derived each window (hoisted: SGPR spills)
         asm volatile("" : "+s"(jl));
-        if (LC > 0) {
-            // the low pairs straight into LDS (lane-linear: pair p of row t at vl[p * TPB + t];
-            // rows outside the basis read zero and are masked where read)
-#pragma unroll
-            for (int p = 0; p < LC / 2; ++p)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    tv, (__attribute__((address_space(3))) void*)(vl + p * TPB + (t & ~63)), 16,
-                    toff + (uint32_t)p * (TPB * 16), 0, 0, 2);
-        }
         // VC: the basis row through the caches (default policy) -- the launcher's choice when
         // this rank's per-step working set fits the 256 MiB Infinity Cache, so the next step
         // re-reads it from there; nt otherwise (streamed once, never re-read in time)
@@ -1230,7 +1141,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                 ql0 = ld(d.RED1, j + l);
             }
         }
-        R.template loadm_even<LC / 2, VC ? 0 : 2>(tv, toff, jl);
+        R.template loadm_even<0, VC ? 0 : 2>(tv, toff, jl);
         // (both loads issued before the patch below waits for the row)
         const double up = inb ? ld(Uin, r) : 0.0;
         const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
@@ -1242,7 +1153,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         double sc, sq;
         if constexpr (FUSE) {
             // (the row loads above are in flight while the reducers of this launch finish)
-            if (a.red) fuse_wait(d.rword, a.wseq, a.werr);
+            if (a.red) fuse_wait(d.rword, a.wseq, a.werr, a.wspin, a.redmm);
             // lane l holds c[l] and q[l]; row_dot2_rl broadcasts them column by column (the same
             // values and FMA order as the scalar-cache form: bitwise the same sums)
             const double hl = ld_ag(d.RED1 + l), gl = ld_ag(d.RED1 + j + l);
@@ -1271,16 +1182,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                 inv_beta = CP4(s1)[D1S_IB];
                 gamma = CP4(s1)[D1S_GAMMA];
             }
-#if TK_D1_COEF_LDS
-        row_dot2_lds<MAXC>(R, cl[0], cl[1], sc, sq);
-#else
-        if constexpr (LC > 0) {
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's LDS columns have landed
-            row_dot2_lc<MAXC, LC>(R, vl, t, inb, c, qv, sc, sq);
-        } else {
             row_dot2<MAXC>(R, c, qv, sc, sq);
-        }
-#endif
         }
         D1_PHASE(0);
         // v_j = (u_j - V c) ib.  With h1 = V'A v_j = (q - Hbar c) ib (CGS's first projection;
@@ -1290,13 +1192,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // (the Hbar c terms cancel): the SpMV is applied to u_j itself, no Hbar is needed
         double* xv = xs[par];
         double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
-#if TK_BK_TEST & 32
-        if (WSC && j > 0) __syncthreads();
-        if (WSC && j > 0) inv_beta = d1s[0], gamma = d1s[1];
-        const double vj = ok ? (up - sc) * inv_beta : 0.0;
-        xv[t] = vj;
-        __syncthreads();
-#else
         double vj = 0.0;
         if constexpr (!WSC) vj = ok ? (up - sc) * inv_beta : 0.0;
         xv[t] = up;
@@ -1308,7 +1203,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             }
             vj = ok ? (up - sc) * inv_beta : 0.0;
         }
-#endif
         const double au = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
         const double u = ok ? inv_beta * (au - sq) - gamma * vj : 0.0;
         D1_PHASE(1);
@@ -1325,8 +1219,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         const double uo = own ? u : 0.0, zo = own ? z : 0.0, vo = own ? vj : 0.0;
         // update_rhs!'s <v_j, b> as norm(b) * <v_j, v_0> (b = norm(b) v_0, src/decompositions.jl:
         // 112-118): v_0 is column 0 of the register row, so b is not read (-8 B per row)
-#define D1_V0R (j > 0 ? (LC > 0 ? (inb ? vl[t].x : 0.0) : R.v[0]) : vj)   // (read where used)
-#ifndef TK_D1_NORED   // (timing experiment: column dots skipped)
+#define D1_V0R (j > 0 ? R.v[0] : vj)   // (read where used)
 #if TK_D1_RS64 && TK_D1_SWPIN
         // rs64's first step on the inputs: the basis entries of columns c and c+4 are
         // half-exchanged once for the u, the z and the Gram products, and each lane forms its
@@ -1338,9 +1231,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         if (gram) swap32(vo, vo, mv1, mv2);
 #pragma unroll
         for (int g = 0; g < (NUZ + 1) / 2; ++g) {
-            // (with LDS columns: this chunk pair's reads are issued here, not hoisted into
-            // one burst that holds them all in registers)
-            if (LC > 0) __builtin_amdgcn_sched_barrier(0);
             double yg[8];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -1349,14 +1239,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                     double y[8], c8[8];
 #pragma unroll
                     for (int i = 0; i < 8; i += 2) {
-                        if (8 * k < LC) {   // (re-read from LDS: the row_dot2 copies are dead)
-                            const d2_t x = vl[(4 * k + (i >> 1)) * TPB + t];
-                            c8[i] = inb ? x.x : 0.0;
-                            c8[i + 1] = inb ? x.y : 0.0;
-                        } else {
-                            c8[i] = R.v[8 * k + i < MAXC ? 8 * k + i : 0];
-                            c8[i + 1] = R.v[8 * k + i + 1 < MAXC ? 8 * k + i + 1 : 0];
-                        }
+                        c8[i] = R.v[8 * k + i < MAXC ? 8 * k + i : 0];
+                        c8[i + 1] = R.v[8 * k + i + 1 < MAXC ? 8 * k + i + 1 : 0];
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -1399,12 +1283,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             }
         }
 #endif
-#endif
         {
 #if TK_D1_RS64 && TK_D1_SWPIN
             // the six scalars in value slots 0..2 (lower half-wave) and 8..10 (upper): three
             // cross-half exchanges, the rest of the first step is zeros
-            if (LC > 0) __builtin_amdgcn_sched_barrier(0);
             const double v0r = D1_V0R;
             double y[8] = {swap_add32(vo * u, uo * z), swap_add32(vo * z, vo * v0r), swap_add32(uo * u, vo * vj)};
             D1_ACC_Y(NUZ, y);
@@ -1772,16 +1654,10 @@ __device__ __forceinline__ void fin_d_tile(const DFac& d, const KArgs& a, int sl
         __syncthreads();
         for (int q = 0; q < tq; q += 2) {
             double x0, x1;
-#if TK_VY_TEST & 2   // (timing experiment: no products)
-            x0 = R.v[q & 7]; x1 = R.v[(q + 1) & 7];
-#elif TK_VY_TEST & 4   // (the scalar-cache form)
-            row_dot2<MAXC>(R, Yf + (int64_t)q * ldy, Yf + (int64_t)(q + 1 < tq ? q + 1 : q) * ldy, x0, x1);
-#else
             row_dot2_lds<MAXC, TK_VY_GRP>(R, Ys + q * ldy, Ys + (q + 1 < tq ? q + 1 : q) * ldy, x0, x1);
-#endif
             // X tile-major like V: the tile's tq columns of 256 rows are one contiguous block,
             // so the stores stream (column-major n x t stores cost a third of the kernel)
-            if (ok && !(TK_VY_TEST & 1)) {
+            if (ok) {
                 double* Xt = Xf + (int64_t)slot * TPB * tq + t;
                 st_x(Xt, (int64_t)q * TPB, x0);
                 if (q + 1 < tq) st_x(Xt, (int64_t)(q + 1) * TPB, x1);
@@ -2241,8 +2117,14 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
     // by the kernel boundary)
     if (t == 0) {
         __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (MM) {
+            // memory-model form: a release store (the windows' fuse_wait takes the acquire);
+            // this thread acquired every block's value at its add above, so the release covers them
+            __hip_atomic_store(d.rword, wseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+            __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 template <bool MM>
@@ -3154,8 +3036,8 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
-    // [ LDS columns (TK_D1_LC) | column-dot slots: (u,z) chunks + scalars (+ Gram chunks) ]
-    size_t lds = ((size_t)D1_LCOLS(M) * TPB + (size_t)(M / 8 + 1 + (gram ? (M + 15) / 16 : 0)) * D1_CHW) * sizeof(double);
+    // column-dot slots: (u,z) chunks + scalars (+ Gram chunks)
+    size_t lds = ((size_t)(M / 8 + 1 + (gram ? (M + 15) / 16 : 0)) * D1_CHW) * sizeof(double);
     if (b.j >= 0) lds = std::max(lds, bk_lds_doubles(b.j) * sizeof(double));
     // (fused with a pending reduce: nf * (3j + 3) leading reducer blocks, rounded to whole XCD rounds)
     const int xr = (fuse && a.red) ? (nf * (3 * a.j + 3) + 7) & ~7 : 0;

@@ -30,6 +30,18 @@ class Context:
         L.check(self._lib.tk_comm_init(self.h, uid, int(nranks), int(rank)))
         self.nranks, self.rank = nranks, rank
 
+    def init_comm_test(self, key, nranks, rank):
+        """Test build only (tests/_build/libtkhip_test.so, loaded through TKHIP_LIB): join an
+        nranks-wide job of processes sharing ONE GPU through the shared-memory stand-in for
+        RCCL (tk_comm_init_test) -- RCCL refuses several ranks on one device."""
+        fn = getattr(self._lib, "tk_comm_init_test", None)
+        if fn is None:
+            raise L.TKError("tk_comm_init_test: %s is not the test build" % L.LIB_PATH)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+        L.check(fn(self.h, key.encode(), int(nranks), int(rank)))
+        self.nranks, self.rank = nranks, rank
+
     def allreduce_host(self, arr):
         arr = np.ascontiguousarray(arr, dtype=np.float64)
         L.check(self._lib.tk_comm_allreduce_host(self.h, L.dptr(arr), arr.size))

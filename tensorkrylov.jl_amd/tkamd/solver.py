@@ -86,7 +86,16 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
                     if eval_overlay is not None and td.part.nranks > 1:
                         sv.share_emulated(td.part.nranks, td.part.rank, eval_overlay)
                 elif _split_wanted(td.part):
-                    sv.share(_share_key(td), td.part.nranks, td.part.rank)
+                    key = _share_key(td)
+                    try:
+                        sv.share(key, td.part.nranks, td.part.rank)
+                    except Exception as e:      # noqa: BLE001  (TKError: no mailbox on this rank)
+                        # continue unsplit: tk_solver_run's agreement at the start of the run
+                        # (max over the ranks of "no mailbox") turns the split off on every rank
+                        import warnings
+                        warnings.warn("evaluation split unavailable on rank %d (%s): every rank "
+                                      "evaluates every iteration" % (td.part.rank, e))
+                        sv.share(key, 1, 0)
                 conv.eval_split = sv.split
                 for j, rec in td.first_records:
                     sv.apply(j, rec)
@@ -156,15 +165,18 @@ def tensorkrylov(conv, A, b, tol, nmax, method, ctx=None, partition=None, verbos
 
 
 def _split_wanted(part):
-    """Evaluation split over the ranks (tk_solver_share): several ranks, all on this node
-    (the mailbox is node-local shared memory; torch.distributed.run sets LOCAL_WORLD_SIZE),
-    not turned off by TKHIP_EVAL_SPLIT=0.  Every rank decides the same way; if a rank still
-    ends up without a mailbox, tk_solver_run's agreement turns the split off everywhere."""
+    """Evaluation split over the ranks (tk_solver_share): several ranks, not turned off by
+    TKHIP_EVAL_SPLIT=0, and every rank positively known to be on this node -- the mailbox is
+    node-local shared memory.  Known means LOCAL_WORLD_SIZE == WORLD_SIZE == the partition's
+    rank count (torch.distributed.run sets both); any other launcher, or a multi-node job,
+    runs unsplit (ranks on other nodes would never find the mailbox).  Every rank
+    decides the same way; if a rank still ends up without a mailbox, it continues unsplit and
+    tk_solver_run's agreement turns the split off everywhere."""
     import os
     if part.nranks <= 1 or os.environ.get("TKHIP_EVAL_SPLIT", "1") == "0":
         return False
     lw, w = os.environ.get("LOCAL_WORLD_SIZE"), os.environ.get("WORLD_SIZE")
-    return lw is None or w is None or lw == w
+    return lw is not None and w is not None and lw == w and int(w) == part.nranks
 
 
 def _share_key(td):

@@ -92,33 +92,88 @@ def test_duplicate_csc_entries_are_summed_like_the_scatter(ctx):
     A.close()
 
 
-def test_failed_step_refuses_later_steps_and_destroys(ctx, monkeypatch):
+def _in_test_build(code, env_extra, timeout=180):
+    """Run `code` in a fresh process on the test build (tests/_build/libtkhip_test.so via
+    TKHIP_LIB): the switches that inject failures exist only there, never in libtkhip.so."""
+    import sys
+    lib = os.path.join(ROOT, "tests", "_build", "libtkhip_test.so")
+    assert os.path.exists(lib), "build() did not produce %s" % lib
+    env = dict(os.environ, TKHIP_LIB=lib, **env_extra)
+    pre = "import sys\nsys.path[:0] = %r\n" % [ROOT, os.path.join(ROOT, "tensorkrylov.jl_amd")]
+    p = subprocess.run([sys.executable, "-c", pre + code], env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p.stdout
+
+
+def test_product_library_has_no_test_switches():
+    """the switches that skip work, drop guards or inject failures are compiled
+    into the test build only."""
+    lib = os.path.join(ROOT, "tensorkrylov.jl_amd", "tkamd", "libtkhip.so")
+    blob = open(lib, "rb").read()
+    for name in (b"TKHIP_TEST_SKIP", b"TKHIP_TEST_XCH_SKIP", b"TKHIP_TEST_NO_GUARD", b"TKHIP_TEST_SHARED_XSIG",
+                 b"TKHIP_TEST_XCH_STALL", b"TKHIP_TEST_FAIL_STEP", b"TKHIP_TEST_FUSE_SPIN", b"tk_comm_init_test"):
+        assert name not in blob, name
+
+
+def test_failed_step_refuses_later_steps_and_destroys():
     """Step 3 reports an injected error on a handle that routes its records through the RCCL
     exchange (1-rank communicator): step 4 and flush are refused with TK_ERR_STATE and
     destroy returns (no exchange left waiting for the failed step's signal)."""
-    tk = _tk()
-    n, K, d = 3000, 10, 2
-    csc = tk.assemble_matrix(n, "Laplace")
-    rng = np.random.default_rng(9)
-    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
-    c2 = tk.Context(0)
-    c2.init_comm(tk.unique_id(), 1, 0)
-    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
-    monkeypatch.setenv("TKHIP_TEST_FAIL_STEP", "3")
-    A = tk.DeviceMatrix(c2, csc)
-    dev = tk.DeviceDecomposition(c2, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
-    dev.init()
-    for j in range(3):
-        dev.step(j)
-    with pytest.raises(tk.TKError, match="injected"):
-        dev.step(3)
-    with pytest.raises(tk.TKError, match="earlier step"):
-        dev.step(4)
-    with pytest.raises(tk.TKError, match="earlier step"):
-        dev.flush()
-    dev.close()
-    A.close()
-    c2.close()
+    out = _in_test_build(r'''
+import numpy as np, pytest
+import tkamd as tk
+n, K, d = 3000, 10, 2
+csc = tk.assemble_matrix(n, "Laplace")
+rng = np.random.default_rng(9)
+bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+c2 = tk.Context(0)
+c2.init_comm(tk.unique_id(), 1, 0)
+A = tk.DeviceMatrix(c2, csc)
+dev = tk.DeviceDecomposition(c2, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+dev.init()
+for j in range(3):
+    dev.step(j)
+with pytest.raises(tk.TKError, match="injected"):
+    dev.step(3)
+with pytest.raises(tk.TKError, match="earlier step"):
+    dev.step(4)
+with pytest.raises(tk.TKError, match="earlier step"):
+    dev.flush()
+dev.close()
+A.close()
+c2.close()
+print("OK")
+''', {"TKHIP_EXCHANGE_ALWAYS": "1", "TKHIP_TEST_FAIL_STEP": "3"})
+    assert out.strip().endswith("OK")
+
+
+def test_fused_wait_that_gives_up_is_reported():
+    """ADVICE r5: a fused one-sweep launch whose bounded wait for its in-launch reducers gives
+    up (forced here: TKHIP_TEST_FUSE_SPIN=1, one poll) sets the context's error word; the
+    records read after the sync then fail with TK_ERR_INTERNAL instead of returning wrong
+    values with TK_OK, and so do tk_ctx_sync and tk_decomp_destroy."""
+    out = _in_test_build(r'''
+import numpy as np, pytest
+import tkamd as tk
+ctx = tk.Context(0)
+n, K, d = 1 << 17, 24, 4
+csc = tk.assemble_matrix(n, "ConvDiff")
+A = tk.DeviceMatrix(ctx, csc)
+bs = [v / np.linalg.norm(v) for v in (np.random.default_rng(1000 + s).random(n) for s in range(d))]
+dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+assert dev.factor_groups == 2
+dev.init(False)
+dev.sweep(0, K)
+with pytest.raises(tk.TKError, match="gave up"):
+    dev.records(0, K + 1)
+with pytest.raises(tk.TKError, match="gave up"):
+    ctx.sync()
+st = ctx._lib.tk_decomp_destroy(dev.h)      # (released either way; the status says why)
+dev.h = None
+assert st == 8, st                          # TK_ERR_INTERNAL
+print("OK")
+''', {"TKHIP_TEST_FUSE_SPIN": "1", "TKHIP_D1_FUSE": "1"})
+    assert out.strip().endswith("OK")
 
 
 @pytest.mark.parametrize("comm", [False, True])
@@ -197,40 +252,42 @@ def test_replica_sends_zero_rows_and_splits_terms(ctx, method, monkeypatch):
         assert np.abs(Xr[f] - ref).max() <= 1e-14 * np.abs(ref).max()
 
 
-def test_exchange_wait_has_a_deadline(monkeypatch):
-    """A records exchange that never completes (TKHIP_TEST_XCH_STALL: the all-reduce of the
-    group holding slot 7 (slots 5..8) waits on a word nobody writes -- a peer that never joins) ends in
-    TK_ERR_RCCL after TKHIP_WAIT_S, naming the slot / step and RCCL's state, instead of
-    spinning forever; afterwards the communicator refuses further collectives at once and
-    destroy returns (its buffers are left to process exit).  1-rank communicator."""
-    import time
-    tk = _tk()
-    n, K, d = 3000, 12, 2
-    csc = tk.assemble_matrix(n, "Laplace")
-    rng = np.random.default_rng(11)
-    bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
-    c = tk.Context(0)
-    c.init_comm(tk.unique_id(), 1, 0)
-    monkeypatch.setenv("TKHIP_EXCHANGE_ALWAYS", "1")
-    monkeypatch.setenv("TKHIP_TEST_XCH_STALL", "7")
-    monkeypatch.setenv("TKHIP_WAIT_S", "2")
-    A = tk.DeviceMatrix(c, csc)
-    dev = tk.DeviceDecomposition(c, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
-    dev.init(False)
-    dev.sweep(0, K)                             # enqueues without waiting
-    r1 = dev.records(1, 5)                      # slots 1..4 went out before the stalled group
-    assert r1.shape == (4, d, dev.m) and (r1[:, :, dev.layout.beta] > 0).all()
-    t0 = time.time()
-    with pytest.raises(tk.TKError, match=r"error 5: records exchange: not complete after 2 s \(record slot 7 = step 6"):
-        dev.records(7, 8)
-    assert time.time() - t0 < 30
-    with pytest.raises(tk.TKError, match="communicator is unusable"):
-        dev.flush()
-    t0 = time.time()
-    dev.close()
-    A.close()
-    c.close()
-    assert time.time() - t0 < 30
+def test_exchange_wait_has_a_deadline():
+    """A records exchange that never completes (TKHIP_TEST_XCH_STALL, test build: the
+    all-reduce of the group holding slot 7 (slots 5..8) waits on a word nobody writes -- a peer
+    that never joins) ends in TK_ERR_RCCL after TKHIP_WAIT_S, naming the slot / step and RCCL's
+    state, instead of spinning forever; afterwards the communicator refuses further collectives
+    at once and destroy returns (its buffers are left to process exit).  1-rank communicator."""
+    out = _in_test_build(r'''
+import time
+import numpy as np, pytest
+import tkamd as tk
+n, K, d = 3000, 12, 2
+csc = tk.assemble_matrix(n, "Laplace")
+rng = np.random.default_rng(11)
+bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+c = tk.Context(0)
+c.init_comm(tk.unique_id(), 1, 0)
+A = tk.DeviceMatrix(c, csc)
+dev = tk.DeviceDecomposition(c, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+dev.init(False)
+dev.sweep(0, K)                             # enqueues without waiting
+r1 = dev.records(1, 5)                      # slots 1..4 went out before the stalled group
+assert r1.shape == (4, d, dev.m) and (r1[:, :, dev.layout.beta] > 0).all()
+t0 = time.time()
+with pytest.raises(tk.TKError, match=r"error 5: records exchange: not complete after 2 s \(record slot 7 = step 6"):
+    dev.records(7, 8)
+assert time.time() - t0 < 30
+with pytest.raises(tk.TKError, match="communicator is unusable"):
+    dev.flush()
+t0 = time.time()
+dev.close()
+A.close()
+c.close()
+assert time.time() - t0 < 30
+print("OK")
+''', {"TKHIP_EXCHANGE_ALWAYS": "1", "TKHIP_TEST_XCH_STALL": "7", "TKHIP_WAIT_S": "2"})
+    assert out.strip().endswith("OK")
 
 
 def test_reduce_handoff_self_check(ctx):

@@ -607,3 +607,27 @@ def test_orthogonality_losses_native_edges_and_lower_triangle():
     assert orthogonality_losses_from_gram(np.array([[1.5]]))[0] == 0.5
     out = np.zeros(1)
     assert L.lib().tk_orthogonality_losses(0, L.dptr(out), L.dptr(out)) == 0
+
+
+def test_split_wanted_only_when_node_locality_is_known(monkeypatch):
+    """the evaluation split (a node-local /dev/shm mailbox) is used only when every
+    rank is positively known to be on this node: LOCAL_WORLD_SIZE == WORLD_SIZE == the
+    partition's rank count.  Unset variables (another launcher) or a multi-node job: unsplit."""
+    from tkamd.solver import _split_wanted
+    part = tkamd.Partition(4, 2, 0)
+    for k in ("LOCAL_WORLD_SIZE", "WORLD_SIZE", "TKHIP_EVAL_SPLIT"):
+        monkeypatch.delenv(k, raising=False)
+    assert not _split_wanted(part)                      # no launcher information
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert not _split_wanted(part)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")         # two nodes, one rank each
+    assert not _split_wanted(part)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert _split_wanted(part)
+    monkeypatch.setenv("TKHIP_EVAL_SPLIT", "0")
+    assert not _split_wanted(part)
+    monkeypatch.delenv("TKHIP_EVAL_SPLIT")
+    assert not _split_wanted(tkamd.Partition(4, 1, 0))  # one rank
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert not _split_wanted(part)                      # the partition is not the launcher's world
