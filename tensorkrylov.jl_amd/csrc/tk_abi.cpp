@@ -342,9 +342,13 @@ static tk_status werr_check(const tk_ctx* c, const char* what) {
 // number s: wait until every rank has consumed s-2 (the buffer's last use), copy this rank's
 // contribution in, post s, wait for every rank's post of s, combine in rank order (sum or
 // max: the records exchange adds zeros to each row, so the sum is exact), consume s.  The
-// records exchange stays stream-ordered on the exchange stream: send rows -> pinned host
-// (hipMemcpyAsync), the combine in a host function (hipLaunchHostFunc), result -> the receive
-// buffer; every rank issues the same collectives in the same order (tk_xsched.h), so the
+// records exchange stays stream-ordered on the exchange stream: send rows -> host-mapped
+// coherent memory, the combine in a host function (hipLaunchHostFunc), result -> the receive
+// buffer.  The two copies are k_mirror_records launches (device-side loads through L2,
+// system-scope stores), not hipMemcpyAsync: a DMA engine reads HBM behind the L2, where a
+// LanczosReorth step's records -- released at device scope only (its exchange waits on an
+// event without a system fence) -- are not yet written back.  Every rank issues the same
+// collectives in the same order (tk_xsched.h), so the
 // sequence numbers agree.  Host all-reduces (preflight, agreements) wait for the exchange
 // stream first and combine on the host directly.  Every wait is bounded by TKHIP_WAIT_S.
 #if TK_TEST_BUILD
@@ -369,9 +373,10 @@ struct TestComm {
     int nranks = 1, rank = 0;
     size_t cap = 0;                     // doubles per buffer
     unsigned long long seq = 0;         // collectives issued by this process
-    double* hsend = nullptr;            // pinned staging of the records exchange
+    double* hsend = nullptr;            // host-mapped staging of the records exchange
     double* hrecv = nullptr;
     size_t hcap = 0;
+    unsigned long long* hword = nullptr;   // (the copy kernels' done word: unused)
     std::atomic<int> failed{0};         // a wait expired inside a host function
     TcRank* rk(int q) const {
         return (TcRank*)((char*)hdr + sizeof(TcHdr) + (size_t)q * (sizeof(TcRank) + 2 * cap * sizeof(double)));
@@ -446,6 +451,8 @@ static void tc_job_cb(void* arg) {
 static tk_status tc_exchange(tk_ctx* c, const double* s, double* r, size_t tot, hipStream_t st) {
     TestComm* tc = c->tcomm;
     if (tc->failed.load()) return wait_expired(c, "records exchange (test transport)", -1);
+    const unsigned flags = hipHostMallocMapped | hipHostMallocCoherent;
+    if (!tc->hword) HIPCHK(hipHostMalloc((void**)&tc->hword, 64, flags));
     if (tot > tc->hcap) {
         tk_status sb = sync_bounded(c, st, "test transport staging");
         if (sb) return sb;
@@ -453,19 +460,21 @@ static tk_status tc_exchange(tk_ctx* c, const double* s, double* r, size_t tot, 
         if (tc->hrecv) hipHostFree(tc->hrecv);
         tc->hsend = tc->hrecv = nullptr;
         tc->hcap = 0;
-        HIPCHK(hipHostMalloc((void**)&tc->hsend, tot * sizeof(double), hipHostMallocDefault));
-        HIPCHK(hipHostMalloc((void**)&tc->hrecv, tot * sizeof(double), hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&tc->hsend, tot * sizeof(double), flags));
+        HIPCHK(hipHostMalloc((void**)&tc->hrecv, tot * sizeof(double), flags));
         tc->hcap = tot;
     }
     TcJob* jb = new TcJob{tc, tot, tc->seq + 1};
     tc->seq += tc_nseq(tc, tot);
-    HIPCHK(hipMemcpyAsync(tc->hsend, s, tot * sizeof(double), hipMemcpyDeviceToHost, st));
+    launch_mirror_records(s, tc->hsend, (int)tot, tc->hword, 1, tc->seq, st);
+    LAUNCHCHK("test transport: send rows to the host");
     hipError_t e = hipLaunchHostFunc(st, tc_job_cb, jb);
     if (e != hipSuccess) {
         delete jb;
         return fail(TK_ERR_HIP, "hipLaunchHostFunc: %s", hipGetErrorString(e));
     }
-    HIPCHK(hipMemcpyAsync(r, tc->hrecv, tot * sizeof(double), hipMemcpyHostToDevice, st));
+    launch_mirror_records(tc->hrecv, r, (int)tot, tc->hword, 1, tc->seq, st);
+    LAUNCHCHK("test transport: combined rows to the device");
     return TK_OK;
 }
 static void tc_destroy(tk_ctx* c) {
@@ -473,6 +482,7 @@ static void tc_destroy(tk_ctx* c) {
     if (!tc) return;
     if (tc->hsend) hipHostFree(tc->hsend);
     if (tc->hrecv) hipHostFree(tc->hrecv);
+    if (tc->hword) hipHostFree(tc->hword);
     if (tc->hdr) munmap(tc->hdr, tc->bytes);
     delete tc;
     c->tcomm = nullptr;
@@ -2588,12 +2598,18 @@ tk_status tk_decomp_records(tk_decomp* dc, int s0, int s1, double* out) { TK_API
         return werr_check(c, "tk_decomp_records");
     }
     if (dc->cstream && dc->recv != dc->rec) {
-        // multi-rank: the slots are final once the exchange of the last one has run
-        // (exchanges run in slot order on the exchange stream); copy on a stream of its own
-        tk_status st = event_bounded(c, dc->ev_x[dc->xev[s1 - 1]], "records exchange", s1 - 1);
-        if (st) {
-            release_stall(dc);
-            return st;
+        // multi-rank: the slots are final once the exchange of the last one SENT in this
+        // sequence has run (exchanges run in slot order on the exchange stream); copy on a
+        // stream of its own.  A slot past xs.sent (e.g. a flush slot no flush filled) has no
+        // exchange: waiting on its never-recorded event returned at once and the copy could
+        // overtake the last real exchange (found by the multi-process test, round 6)
+        const int w = std::min(s1 - 1, dc->xs.sent);
+        if (w >= s0) {
+            tk_status st = event_bounded(c, dc->ev_x[dc->xev[w]], "records exchange", w);
+            if (st) {
+                release_stall(dc);
+                return st;
+            }
         }
         HIPCHK(hipMemcpyAsync(out, dc->recv + s0 * per, (s1 - s0) * per * sizeof(double), hipMemcpyDeviceToHost,
                               dc->cstream));
