@@ -1133,6 +1133,14 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // first) and every wave evaluates them (d1_scalars); step 0 reads the init's
         const int l = t & 63;
         double cl0 = 0.0, ql0 = 0.0;
+        double* xv = xs[par];
+        double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
+        // u_j (and column j-1 from E) first, then the basis row: A u_j needs only u_j, so the
+        // first SpMV (its barrier and LDS reads) runs while the row's loads are in flight, and
+        // the row is waited for at the projections row . c, row . q that follow (round 6, same
+        // box: C2 +1..3 %, C4 N = 8 rank 0 +8 %, rank 7 +3..8 %; profiles/r06/early_spmv_ab.txt)
+        const double up = inb ? ld(Uin, r) : 0.0;
+        const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
         if constexpr (!FUSE) {
             // (wave 0 evaluates them for the block and hands them on through LDS at the barrier
             // before the SpMV, the first place that needs them: one 1 KB load per block)
@@ -1141,16 +1149,28 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
                 ql0 = ld(d.RED1, j + l);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);
         R.template loadm_even<0, VC ? 0 : 2>(tv, toff, jl);
-        // (both loads issued before the patch below waits for the row)
-        const double up = inb ? ld(Uin, r) : 0.0;
-        const double e = (inb && (j & 1)) ? ld(d.E, r) : 0.0;
-        if (j & 1) R.set_col(j - 1, e);
+        __builtin_amdgcn_sched_barrier(0);
         // (step 0: ib, gamma of the init, k_post; with factor groups the reduce's last block
         // stored them after the values)
         const double* s1 = d.RED1 + (j > 0 ? 3 * j + 3 : 2);
         double inv_beta, gamma;
         double sc, sq;
+        if constexpr (!FUSE) {
+            if (WSC && j > 0 && t < 64) {
+                double beta, ib, t1;
+                d1_scalars(cl0, ql0, CP4(d.RED1)[2 * j], CP4(d.RED1)[2 * j + 1], beta, ib, t1);
+                if (t == 0) {
+                    d1s[0] = ib;
+                    d1s[1] = t1 * ib;
+                }
+            }
+        }
+        xv[t] = up;
+        __syncthreads();
+        const double au = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
+        if (j & 1) R.set_col(j - 1, e);
         if constexpr (FUSE) {
             // (the row loads above are in flight while the reducers of this launch finish)
             if (a.red) fuse_wait(d.rword, a.wseq, a.werr, a.wspin, a.redmm);
@@ -1169,15 +1189,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             row_dot2_rl<MAXC>(R, hl, gl, sc, sq);
         } else {
             if (WSC && j > 0) {
-                inv_beta = gamma = 0.0;   // (from d1s after the barrier below)
-                if (t < 64) {
-                    double beta, ib, t1;
-                    d1_scalars(cl0, ql0, CP4(d.RED1)[2 * j], CP4(d.RED1)[2 * j + 1], beta, ib, t1);
-                    if (t == 0) {
-                        d1s[0] = ib;
-                        d1s[1] = t1 * ib;
-                    }
-                }
+                inv_beta = d1s[0];
+                gamma = d1s[1];
             } else {
                 inv_beta = CP4(s1)[D1S_IB];
                 gamma = CP4(s1)[D1S_GAMMA];
@@ -1190,20 +1203,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // relation A V c = V Hbar c turns CGS's
         //   u_{j+1} = A v_j - V h1[0..j) - h1[j] v_j   into   ib (A u_j - V q) - gamma v_j
         // (the Hbar c terms cancel): the SpMV is applied to u_j itself, no Hbar is needed
-        double* xv = xs[par];
-        double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
-        double vj = 0.0;
-        if constexpr (!WSC) vj = ok ? (up - sc) * inv_beta : 0.0;
-        xv[t] = up;
-        __syncthreads();
-        if constexpr (WSC) {
-            if (j > 0) {
-                inv_beta = d1s[0];
-                gamma = d1s[1];
-            }
-            vj = ok ? (up - sc) * inv_beta : 0.0;
-        }
-        const double au = ok ? spmv<FMT>(d.A, r, [&](int64_t cc) { return xv[clamp_row(cc - S)]; }) : 0.0;
+        const double vj = ok ? (up - sc) * inv_beta : 0.0;
         const double u = ok ? inv_beta * (au - sq) - gamma * vj : 0.0;
         D1_PHASE(1);
         xu[t] = u;
