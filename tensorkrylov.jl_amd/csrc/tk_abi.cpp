@@ -1445,7 +1445,9 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.b = bb;
         DA(d.W, (size_t)dc->ld * sizeof(double));
         DA(d.U, (size_t)dc->ld * sizeof(double));
-        DA(d.P1, (size_t)dc->nvmax * npp * sizeof(double));
+        // (one-sweep Arnoldi: window-major groups of D1G values, nvmax rounded up to whole groups)
+        const size_t nvp = (size_t)d1_groups(dc->nvmax) * D1G;
+        DA(d.P1, nvp * npp * sizeof(double));
         DA(d.P2, (size_t)dc->nvmax * npp * sizeof(double));
         DA(d.RED1, (size_t)std::max(dc->nvmax, RED1_LEN(kmax)) * sizeof(double));
         DA(d.RED2, (size_t)dc->nvmax * sizeof(double));
@@ -1455,11 +1457,17 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         DA(d.H, (size_t)KP * KC * sizeof(double));
         DA(d.lossrow, (size_t)KP * sizeof(double));
         DA(d.ctr, 16);
+        d.Q = nullptr;
+        d.ctrg = nullptr;
+        if (dc->onesweep && method == TK_ARNOLDI) {
+            DA(d.Q, (size_t)d1_groups(dc->nvmax) * 16 * D1G * sizeof(double));
+            DA(d.ctrg, (size_t)d1_groups(dc->nvmax) * sizeof(unsigned int));   // (zeroed by dalloc)
+        }
         DA(d.E, (size_t)(dc->onesweep ? dc->ld : 1) * sizeof(double));
         d.P1b = nullptr;
         d.rword = nullptr;
         if (dc->fuse) {
-            DA(d.P1b, (size_t)dc->nvmax * npp * sizeof(double));
+            DA(d.P1b, nvp * npp * sizeof(double));
             DA(d.rword, 64);   // (zeroed by dalloc; step words start at 1)
         }
         const int gi = first_factor + f;
@@ -1886,6 +1894,7 @@ static KArgs base_args(tk_decomp* dc, int j, int slot) {
     a.wseq = 0;
     a.werr = nullptr;
     a.wspin = fuse_spin();
+    a.pgrp = 0;
     a.wsc = 0;
     a.xval = 0;
     return a;
@@ -2009,6 +2018,17 @@ static tk_status clear_slot(tk_decomp* dc, int slot) {
 // loads the basis with the default cache policy instead of nt (0: always nt).  The Infinity
 // Cache is 256 MiB; a line stays resident while everything touched between two uses fits, and
 // past it the cached loads still paid up to ~450 MB (the A/B in profiles/r05/)
+// TKHIP_D1_PGRP_MIN: the smallest window count per factor for window-major partials with
+// factor groups (2048: C2's 4 162 windows use them, C1's 1 050 do not; 0 = always, a huge value =
+// never)
+static int d1_pgrp_min() {
+    static const int v = [] {
+        const char* e = getenv("TKHIP_D1_PGRP_MIN");
+        return e ? std::max(0, atoi(e)) : 2048;
+    }();
+    return v;
+}
+
 static double d1_cache_bytes() {
     static const double v = [] {
         const char* e = getenv("TKHIP_D1_CACHE_MB");
@@ -2215,6 +2235,14 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
         // one stream: the reduce is a plain reduction and the windows evaluate the scalars;
         // with factor groups the reduce's last block does (hidden behind the other group)
         a.wsc = grouped ? 0 : 1;
+        // factor groups over long grids (no fused launches): window-major partials, written as
+        // whole lines, and their two-level reduce (its extra hand-off hidden behind the other
+        // group's sweep); short grids and one stream keep value-major partials and the one-level
+        // reduce.  Both sum in the same order: bitwise the same results.  Same box, two reps
+        // (profiles/r06/window_major_partials_ab.txt): C2 N = 1 +1.9 / +2.6 %, the other lines
+        // within the box noise; window-major on every grouped grid (TKHIP_D1_PGRP_MIN=0): C1
+        // +3.5 / -1.4 %
+        a.pgrp = (grouped && !dc->fuse && dc->npd >= d1_pgrp_min()) ? 1 : 0;
         KArgs b = base_args(dc, -1, slot);
         b.j = -1;
         if (dc->bk_j >= 0 && dc->bk_j == j - 1 && dc->bk_kind == 0) b = dc->bk_args;
@@ -2265,7 +2293,8 @@ static tk_status step_impl(tk_decomp* dc, int j, double* rec_out) {
                 if (!(dc->skip_mask & 1) && !dc->fuse) {
                     Timer tm_(c, TCLS_RED, 2, sg);
                     HpScope hp_(HP_RED);
-                    launch_reduce(dc->df + g0, ng, 1, 3 * j + 6, 0, sg, 0, j + 1);
+                    if (a.pgrp) launch_red_d1(dc->df + g0, ng, 1, j + 1, dc->npd, sg);
+                    else launch_reduce(dc->df + g0, ng, 1, 3 * j + 6, 0, sg, 0, j + 1);
                 }
                 LAUNCHCHK("reduce");
             }

@@ -77,9 +77,13 @@ struct DFac {
     double* Uint;
     double* AU;
     int ifs, inf;
-    // one-sweep reduce: arrival counter of the step's value blocks (the last one evaluates
-    // the next step's scalars, k_reduce256)
+    // one-sweep reduce: arrival counter of the step's value groups (the last one evaluates
+    // the next step's scalars, red_d1_block)
     unsigned int* ctr;
+    // one-sweep reduce, first level: each group's per-split sums ([group][split][16]) and the
+    // group's arrival counter (the last split block of a group sums the splits in order)
+    double* Q;
+    unsigned int* ctrg;
     // fused one-sweep launches (the previous step's reduce in the leading blocks): the odd
     // steps' partials, and the step word the reducers publish and the window blocks wait for
     double* P1b;
@@ -125,6 +129,8 @@ struct KArgs {
     // the windows evaluate the next step's scalars (d1_scalars); 0: the reduce's last block does
     // and stores them (with two group streams that reduce hides behind the other group's sweep)
     int wsc;
+    int pgrp;         // one-sweep Arnoldi, factor groups without fused launches: the window partials
+                      // in window-major groups (D1G) and their reduce red_d1_block; 0: value-major
 };
 
 // One-sweep Arnoldi steps j <= D1_JMAX (the j basis columns it reads fit the register
@@ -136,6 +142,16 @@ constexpr int ARN_D1_JMAX = 63;
 // RED1 length: 3 kmax + 8 reduced values, plus the span one-sweep register rows read past
 // the live coefficients (2 x 64 + 16)
 #define RED1_LEN(kmax) (3 * (kmax) + 8 + 144)
+// One-sweep Arnoldi partials (k_arn_d1 -> red_d1_block): window-major groups of D1G values, group
+// g of window w at P1[(g * npd + w) * D1G + v % D1G] -- each window stores every group as one
+// whole 128-byte line (16 lanes of one instruction) -- on factor groups over long grids
+// (KArgs::pgrp); value-major P1[v * npd + w] elsewhere.  Both reduces sum in the same order
+// (red_d1_block emulates red256_block's), so the layout never changes a bit of the results.
+#define D1G 16
+__host__ __device__ inline int d1_groups(int nv) { return (nv + D1G - 1) / D1G; }
+// values the reduce of one-sweep Arnoldi step J - 1 sums (J = coefJ): c and q (J each), |u|^2,
+// <u,z>, <v,v_0>, the Gram diagonal, and a tracked factor's Gram row (J - 1)
+__host__ __device__ inline int d1_nv(int J, int track_gram) { return track_gram ? 3 * J + 3 : 2 * J + 4; }
 // launch_reduce's coefJ for a one-sweep Lanczos step (k_lan_1s)
 #define RED_LAN (-2)
 // where a one-sweep step's reduced dots (3j+6 values) are followed by the next step's
@@ -194,6 +210,9 @@ void launch_lan_finalize(const DFac* F, int nf, const KArgs& a, hipStream_t s);
 // one partial per tile (reduce with npart = ntiles)
 void launch_fin_d(const DFac* F, int nf, const KArgs& a, int mode, hipStream_t s);
 // npart <= 0: each factor's own DFac::npd partials (one-sweep Arnoldi)
+// the one-sweep Arnoldi step's reduce of step J - 1 over window-major partials (KArgs::pgrp,
+// red_d1_block); npd: the launch's largest window count
+void launch_red_d1(const DFac* F, int nf, int which, int J, int npd, hipStream_t s);
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate = 0,
                    int coefJ = -1, const KArgs* ax = nullptr);
 // post-processing (one 64-thread block per factor)

@@ -1042,7 +1042,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // evaluates the step's scalars (d1_scalars) and hands them to the block through LDS
     constexpr bool WSC = (MODE & 4) != 0 && !FUSE;
     __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
-    __shared__ double d1s[WSC ? 2 : 1];                // the step's ib, gamma (wave 0 -> the block)
+    __shared__ double d1s[2];                          // the step's ib, gamma (wave 0 -> the block; WSC)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const DFac& d = F[blockIdx.y];
 #if TK_D1_ONEWIN
@@ -1106,6 +1106,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const bool gram = d.track_gram != 0;
     const int nch = NUZ + 1 + (gram ? NG : 0);
     for (int e = t; e < nch * D1_CHW; e += TPB) acc[e] = 0.0;   // private slots
+    // KArgs::pgrp: the window's reduced values by value index, stored as whole groups at the end
+    __shared__ double pv[D1G * ((3 * 64 + 6 + D1G - 1) / D1G)];
+    const bool pg = !FUSE && a.pgrp;
+    const int nvp = pg ? d1_groups(d1_nv(j + 1, gram)) * D1G : 0;
+    for (int e = t; e < nvp; e += TPB) pv[e] = 0.0;
     int par = 0;
 #if TK_D1_ONEWIN
     // one window per block (no window loop: nothing loop-invariant to hoist)
@@ -1326,7 +1331,19 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
 #endif
             if (col < j) vi = 2 * j + 6 + col;
         }
-        if (vi >= 0) st_wt((FUSE && (j & 1)) ? d.P1b : d.P1, (int64_t)vi * d.npd + slot, sum);
+        if (vi >= 0) {
+            if (pg) pv[vi] = sum;
+            else st_wt((FUSE && (j & 1)) ? d.P1b : d.P1, (int64_t)vi * d.npd + slot, sum);
+        }
+    }
+    if (pg) {
+        // window-major groups of D1G values (tk_internal.h): each group one whole 128-byte line
+        // from 16 lanes of one store instruction.  Value-major partials (one 8-byte write per value
+        // and window, each its own transaction) cost ~10 % of the step's memory time in the traffic
+        // probe (profiles/r06/d1probe_store_variants.txt); whole lines recover most of it, for a
+        // heavier reduce (red_d1_block) -- where it is hidden: factor groups over long grids
+        __syncthreads();
+        for (int e = t; e < nvp; e += TPB) st_wt(d.P1, ((int64_t)(e / D1G) * d.npd + slot) * D1G + (e % D1G), pv[e]);
     }
 #if TK_D1_TRACE
     __syncthreads();
@@ -2126,6 +2143,104 @@ __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int
             __hip_atomic_store(d.rword, wseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+}
+// The one-sweep Arnoldi step's reduce over window-major partials (KArgs::pgrp: factor groups
+// over long grids; groups of D1G values, tk_internal.h), in EXACTLY the arithmetic order of the
+// value-major reduce (red256_block), so that the layout a launch uses never changes a bit.  There,
+// lane t of a value's block sums windows t, t + 256, t + 512, ... in order, the 16 lanes of each
+// DPP row combine through row16_sum (rotations by 8, 4, 2, 1; lane 0's result is kept) and the 16
+// row results are summed in order.  Here block `bid` = (group g, row q) takes lanes 16q .. 16q+15
+// of all D1G values of the group (a wave loads four windows' whole 128-byte lines per
+// instruction), evaluates row16_sum's tree for lane 0 of the row, stores the D1G row results to Q
+// and counts its arrival on the group's counter; the group's last row block sums the 16 rows in
+// order into RED1.  The factor's last group (a second counter) evaluates the next step's scalars
+// (d1_scalars) and stores them after the values, as k_reduce256's last block does.
+// Hand-offs: the relaxed form of the measured table in /opt/skills/guides/MI355X_MICROARCH.md
+// (every handed-off value stored sc1 by the adding lane's own wave, drained with vmcnt(0) before
+// the add; every reader loads sc1 after its add returned), or with MM the memory-model form
+// (acq_rel adds, an acquire fence in the last block).
+template <bool MM>
+__device__ __forceinline__ void red_d1_block(const DFac& d, int bid, int which, int J) {
+    __shared__ double sv[TPB];
+    __shared__ int last;
+    const int nvr = d1_nv(J, d.track_gram), ng = d1_groups(nvr);
+    if (bid >= ng * 16) return;
+    const int g = bid >> 4, row = bid & 15;
+    const double* P = (which == 5 ? d.P1b : d.P1) + (int64_t)g * d.npd * D1G;
+    const int t = threadIdx.x, v = t % D1G, tl = t / D1G, lane = 16 * row + tl;
+    const int npart = d.npd;
+    double s = 0.0;
+    for (int b0 = 0; b0 < npart; b0 += 6144) {   // (red256_block's rounds, zeros past the end included)
+        double part[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            const int b = b0 + lane + 256 * i;
+            part[i] = b < npart ? ld(P, (int64_t)b * D1G + v) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 24; ++i) s += part[i];
+    }
+    sv[tl * D1G + v] = s;
+    __syncthreads();
+    auto cld = [&](const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    if (t < D1G) {
+        // row16_sum's lane 0: x_i = s_i + s_{i+8}, y_i = x_i + x_{i+4}, z_i = y_i + y_{i+2},
+        // w_0 = z_0 + z_1 (each rotation adds the lane's own value first; IEEE addition commutes)
+        double x[8], y[4], z[2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x[i] = sv[i * D1G + t] + sv[(i + 8) * D1G + t];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) y[i] = x[i] + x[i + 4];
+        z[0] = y[0] + y[2];
+        z[1] = y[1] + y[3];
+        __hip_atomic_store(d.Q + ((int64_t)g * 16 + row) * D1G + t, z[0] + z[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 0) {   // (lanes 0..15 of this wave stored the rows)
+        if constexpr (MM) {
+            last = __hip_atomic_fetch_add(d.ctrg + g, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 15u;
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+            last = __hip_atomic_fetch_add(d.ctrg + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 15u;
+        }
+    }
+    __syncthreads();
+    if (!last) return;
+    if constexpr (MM) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (t < D1G) {
+        double r = 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) r += cld(d.Q + ((int64_t)g * 16 + q) * D1G + t);
+        if (g * D1G + t < nvr) __hip_atomic_store(d.RED1 + g * D1G + t, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // (the counter's reset is ordered before the next reduce by the kernel boundary)
+    if (t == 0) __hip_atomic_store(d.ctrg + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the factor's groups: the last one to finish evaluates the scalars
+    if (t == 0) {   // (lanes 0..15 of this wave stored the values)
+        if constexpr (MM) {
+            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ng - 1);
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+            last = __hip_atomic_fetch_add(d.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(ng - 1);
+        }
+    }
+    __syncthreads();
+    if (!last || t >= 64) return;
+    if constexpr (MM) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double beta, ib, t1;
+    d1_scalars(t < J ? cld(d.RED1 + t) : 0.0, t < J ? cld(d.RED1 + J + t) : 0.0, cld(d.RED1 + 2 * J),
+               cld(d.RED1 + 2 * J + 1), beta, ib, t1);
+    if (t == 0) {
+        double* o = d.RED1 + 3 * J + 3;
+        st(o, D1S_IB, ib);
+        st(o, D1S_GAMMA, t1 * ib);
+        st(o, D1S_BETA, beta);
+        st(o, D1S_T1, t1);
+        __hip_atomic_store(d.ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+template <bool MM>
+__global__ __launch_bounds__(256) void k_red_d1(const DFac* __restrict__ F, int which, int J) {
+    red_d1_block<MM>(F[blockIdx.y], (int)blockIdx.x, which, J);
 }
 template <bool MM>
 __global__ __launch_bounds__(256) void k_reduce256(const DFac* __restrict__ F, int which, int nv, int np,
@@ -3030,9 +3145,10 @@ void launch_lan_1w(const DFac* F, int nf, const KArgs& a, const KArgs& b, int np
         else hipLaunchKernelGGL((k_lan_1w<decltype(FM)::value, false>), grid, dim3(TPB), 64 * sizeof(double), s, F, a, b);
     });
 }
-void launch_arn_d1(const DFac* F, int nf, const KArgs& a, const KArgs& b, int npd, bool gram, bool vcache,
+void launch_arn_d1(const DFac* F, int nf, const KArgs& a0, const KArgs& b, int npd, bool gram, bool vcache,
                    bool fuse, hipStream_t s) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
+    const KArgs& a = a0;
     // per-lane accumulators: register-row chunks (u,z) + scalars + Gram chunks; with the
     // previous step's bookkeeping (b.j >= 0) at least its Hbar + reduced dots
     const int M = a.j <= 8 ? 8 : (a.j + 7) / 8 * 8;
@@ -3122,6 +3238,13 @@ static std::atomic<int> g_red_mm{TK_RED_MM};
 int red_mm() { return g_red_mm.load(std::memory_order_relaxed); }
 void set_red_mm(int on) { g_red_mm.store(on ? 1 : 0, std::memory_order_relaxed); }
 
+void launch_red_d1(const DFac* F, int nf, int which, int J, int npd, hipStream_t s) {
+    if (nf <= 0) return;   // (a rank that owns no factors launches nothing)
+    (void)npd;
+    const dim3 grid(d1_groups(d1_nv(J, 1)) * 16, nf);
+    if (red_mm()) hipLaunchKernelGGL(k_red_d1<true>, grid, dim3(256), 0, s, F, which, J);
+    else hipLaunchKernelGGL(k_red_d1<false>, grid, dim3(256), 0, s, F, which, J);
+}
 void launch_reduce(const DFac* F, int nf, int which, int nv, int npart, hipStream_t s, int gate, int coefJ,
                    const KArgs* ax) {
     if (nf <= 0) return;   // (a rank that owns no factors launches nothing)

@@ -6,6 +6,8 @@ the steps are taken one at a time with their records (the driver's pattern) or a
 and for an odd factor count (groups of 2 and 3).  Reference: the per-factor steps of
 orthonormalize! (src/orthogonal_bases.jl:162-180) are independent of each other.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -290,3 +292,55 @@ def test_lanczos_single_column_layout_bitwise_equal_pairs(ctx, d, K, monkeypatch
         assert a[i].shape == b[i].shape
         assert np.abs(a[i] - b[i]).max() <= 1e-13
         assert np.abs(np.diag(b[i]) - 1.0).max() < 1e-8
+
+
+@pytest.mark.parametrize("n", [3000, 1 << 18, 1 << 20])
+def test_window_major_partials_bitwise_equal_value_major(ctx, n, monkeypatch):
+    """Round 6: factor groups over long grids store the one-sweep Arnoldi step's window partials
+    window-major (each value group one whole 128-byte line) and reduce them in two levels
+    (red_d1_block); one stream and fused launches keep value-major partials (red256_block).  Both
+    reduces sum in the same order, so the layout never changes a bit: the records and bases of a
+    grouped handle with window-major partials (forced at every size in a subprocess,
+    TKHIP_D1_PGRP_MIN=0; one split at n = 3000, several at 2^18 and 2^20) equal those of a
+    one-stream handle of the same factors, bit for bit."""
+    import hashlib
+    import json
+    import subprocess
+    import sys
+    tk = __import__("tkamd")
+    d, K = 3, 30
+    code = r'''
+import hashlib, json, sys
+sys.path[:0] = %r
+import numpy as np
+import tkamd as tk
+n, d, K = %d, %d, %d
+ctx = tk.Context(0)
+mats = [tk.DeviceMatrix(ctx, tk.assemble_matrix(n, c)) for c in ("Laplace", "ConvDiff")]
+bs = [v / np.linalg.norm(v) for v in (np.random.default_rng(1000 + s).random(n) for s in range(d))]
+dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, d, 0, [mats[s %% 2] for s in range(d)], bs, K)
+assert dev.factor_groups == 2 and dev.arnoldi_sweeps == 1
+dev.init(False)
+dev.sweep(0, K)
+rec = dev.records(0, K + 1)
+V = [hashlib.sha256(dev.basis(s, 0, K).tobytes()).hexdigest() for s in range(d)]
+print(json.dumps({"rec": hashlib.sha256(rec.tobytes()).hexdigest(), "V": V}))
+''' % (sys.path, n, d, K)
+    env = dict(os.environ, TKHIP_D1_PGRP_MIN="0")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    monkeypatch.setenv("TKHIP_FACTOR_GROUPS", "1")
+    mats = [tk.DeviceMatrix(ctx, tk.assemble_matrix(n, c)) for c in ("Laplace", "ConvDiff")]
+    bs = [v / np.linalg.norm(v) for v in (np.random.default_rng(1000 + s).random(n) for s in range(d))]
+    dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, d, 0, [mats[s % 2] for s in range(d)], bs, K)
+    assert dev.factor_groups == 1
+    dev.init(False)
+    dev.sweep(0, K)
+    rec = dev.records(0, K + 1)
+    V = [hashlib.sha256(dev.basis(s, 0, K).tobytes()).hexdigest() for s in range(d)]
+    dev.close()
+    for m in mats:
+        m.close()
+    assert got["rec"] == hashlib.sha256(rec.tobytes()).hexdigest()
+    assert got["V"] == V
