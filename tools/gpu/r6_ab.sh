@@ -9,8 +9,10 @@ for rep in $REPS; do for cs in $CASES; do
   EM=""; [ "$N" != 1 ] && EM="--emulate-ranks $N --emulate-rank $RK"
   for v in tree "$@"; do
     # (a variant "VAR=VAL" runs the in-tree library with that environment variable)
-    L=""; case "$v" in tree) ;; *=*) L="$v" ;; *) L="TKHIP_LIB=$R/tools/_build/libtkhip_$v.so" ;; esac
-    log=gpurun_out/ab_${v//=/_}_${CFG}_${N}_${RK}_$rep.log
+    # ("A=1,B=2": several)
+    L=""; case "$v" in tree) ;; *=*) L="${v//,/ }" ;; *) L="TKHIP_LIB=$R/tools/_build/libtkhip_$v.so" ;; esac
+    vn=${v//=/_}; vn=${vn//,/_}
+    log=gpurun_out/ab_${vn}_${CFG}_${N}_${RK}_$rep.log
     env $L timeout -k 10 200 python bench.py --config $CFG $EM --steps $STEPS --warmup 2 --no-cpu-baseline --no-end-to-end $BARGS > $log 2>&1 || { echo "$v $cs failed"; tail -3 $log; exit 1; }
     tail -1 $log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$rep $cs %-6s' % '$v', d['value'], d['roofline']['avg_launch_us'], d['roofline']['frac'])"
   done

@@ -14,7 +14,7 @@ import json
 import os
 import sys
 
-STEP_KERNELS = ("k_arn_a1", "k_arn_a2", "k_arn_d1", "k_reduce", "k_post", "k_lan_", "k_spmv_mf", "k_ilv")
+STEP_KERNELS = ("k_arn_a1", "k_arn_a2", "k_arn_d1", "k_reduce", "k_red_d1", "k_post", "k_lan_", "k_spmv_mf", "k_ilv")
 GATHER_KERNELS = ("k_spmv_mf",)
 
 
