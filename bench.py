@@ -487,8 +487,11 @@ def main():
             # atomics confirmed by the startup self-check, or the memory-model form
             "reduce_handoff": {0: "relaxed (self-checked against the memory-model form)",
                                1: "memory-model release/acquire",
-                               2: "relaxed (forced, TKHIP_RED_MM=0)"}.get(L.lib().tk_reduce_handoff(),
-                                                                          "not used (no one-sweep step)"),
+                               2: "relaxed (forced, TKHIP_RED_MM=0)",
+                               3: "memory-model release/acquire (the self-check could not run)"}.get(
+                                   L.lib().tk_reduce_handoff(), "not used (no one-sweep step)"),
+            # (its one-off cost inside the first tk_decomp_create of the process, outside the timed region)
+            "reduce_handoff_check_ms": round(L.lib().tk_reduce_check_ms(), 2),
             "end_to_end": e2e,
             "basis_mul_step": {
                 "engine": ("k_fin_vy: flush of the pending column + V*Y from its register row (FP64 FMA), "

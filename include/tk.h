@@ -154,10 +154,14 @@ tk_status tk_decomp_agree(tk_decomp* dc, int* vals, int count);
 /* The one-sweep steps' reduce hand-off: 0 = relaxed agent-scope atomics
  * (measured correct on gfx950, and confirmed by a self-check against the memory-model form at
  * the process's first tk_decomp_create), 1 = the HIP memory model's release/acquire form (kept
- * when the self-check finds any difference or cannot run; TKHIP_RED_MM=0/1 forces a form),
- * 2 = relaxed, forced by TKHIP_RED_MM=0 without the check, -1 = not settled yet (no
+ * when the self-check finds any difference; TKHIP_RED_MM=1 forces it), 2 = relaxed, forced by
+ * TKHIP_RED_MM=0 without the check, 3 = the memory-model form because the self-check could not
+ * run (its context, matrix, decomposition or steps failed), -1 = not settled yet (no
  * decomposition created). */
 int tk_reduce_handoff(void);
+/* Wall time (ms) of that self-check -- a one-off cost of the process's first tk_decomp_create
+ * (0 when it did not run). */
+double tk_reduce_check_ms(void);
 
 /* Multi-rank waits (the records exchange, tk_comm_allreduce_host, tk_ctx_sync, destroy) are
  * bounded by TKHIP_WAIT_S seconds (default 120): on expiry the call returns TK_ERR_RCCL naming

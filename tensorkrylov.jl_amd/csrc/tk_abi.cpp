@@ -1211,7 +1211,10 @@ static void free_decomp(tk_decomp* dc) {
 // bitwise the same records; on any difference -- or if the check cannot run -- the process
 // keeps the memory-model form.  TKHIP_RED_MM=0/1 skips the check and forces
 // a form.  tk_reduce_handoff() reports the outcome.
-static std::atomic<int> g_red_state{0};   // 0 not checked, 1 relaxed (checked), 2 MM (mismatch or failure), 3 forced
+// 0 not checked, 1 relaxed (checked), 2 MM (the forms differed), 3 forced (TKHIP_RED_MM), 4 MM (the
+// check could not run: context, matrix or decomposition creation, or a step, failed)
+static std::atomic<int> g_red_state{0};
+static std::atomic<double> g_red_check_ms{0.0};   // the check's wall time (setup cost of the first create)
 static thread_local bool g_in_red_check = false;
 
 static int red_check_run(int device) {
@@ -1238,7 +1241,7 @@ static int red_check_run(int device) {
     tk_ctx* cc = nullptr;
     tk_mat* A = nullptr;
     tk_decomp* dc = nullptr;
-    int verdict = 2;
+    int verdict = 4;   // (could not run, unless both forms ran)
     std::vector<double> rec[2];
     if (tk_ctx_create(device, &cc) == TK_OK &&
         tk_matrix_from_csc(cc, n, colptr.data(), rowval.data(), nz.data(), 0, &A) == TK_OK) {
@@ -1275,22 +1278,29 @@ static void red_check_once(int device) {
         return;
     }
     g_in_red_check = true;
+    const auto t0 = std::chrono::steady_clock::now();
     const int v = red_check_run(device);
+    g_red_check_ms.store(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     g_in_red_check = false;
     set_red_mm(v == 1 ? 0 : 1);
     if (v != 1)
-        fprintf(stderr, "libtkhip: the relaxed reduce hand-off %s its self-check: using the memory-model form\n",
-                v == 2 ? "failed" : "could not run");
+        fprintf(stderr, "libtkhip: the relaxed reduce hand-off %s: using the memory-model form\n",
+                v == 2 ? "gave other records than the memory-model form in its self-check"
+                       : "self-check could not run");
     g_red_state.store(v);
 }
 
-// 0: the relaxed hand-off, self-checked; 1: the memory-model form; 2: relaxed, forced by
-// TKHIP_RED_MM=0 (no check); -1: not settled yet
+// 0: the relaxed hand-off, self-checked; 1: the memory-model form (the check found a difference, or
+// TKHIP_RED_MM=1); 2: relaxed, forced by TKHIP_RED_MM=0 (no check); 3: the memory-model form because
+// the check could not run; -1: not settled yet
 int tk_reduce_handoff(void) {
     const int st = g_red_state.load();
     if (st <= 0) return -1;
+    if (st == 4) return 3;
     return red_mm() ? 1 : (st == 3 ? 2 : 0);
 }
+
+double tk_reduce_check_ms(void) { return g_red_check_ms.load(); }
 
 tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor, int nf,
                            tk_mat* const* mats, const double* const* b, int64_t n, int kmax,

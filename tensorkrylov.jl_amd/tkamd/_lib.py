@@ -42,6 +42,7 @@ def lib():
         "tk_last_error": (ctypes.c_char_p, []),
         "tk_version": (I, []),
         "tk_reduce_handoff": (I, []),
+        "tk_reduce_check_ms": (ctypes.c_double, []),
         "tk_ctx_create": (I, [I, ctypes.POINTER(P)]),
         "tk_ctx_destroy": (I, [P]),
         "tk_ctx_sync": (I, [P]),
@@ -104,7 +105,7 @@ def lib():
 
 
 # every symbol include/tk.h declares (tests check the .so exports all of them)
-EXPORTS = ("tk_last_error", "tk_version", "tk_reduce_handoff", "tk_ctx_create", "tk_ctx_destroy", "tk_ctx_sync",
+EXPORTS = ("tk_last_error", "tk_version", "tk_reduce_handoff", "tk_reduce_check_ms", "tk_ctx_create", "tk_ctx_destroy", "tk_ctx_sync",
            "tk_comm_unique_id", "tk_comm_init", "tk_comm_allreduce_host", "tk_comm_count",
            "tk_matrix_from_csc", "tk_matrix_from_csr", "tk_matrix_destroy", "tk_matrix_format", "tk_matvec",
            "tk_record_len", "tk_decomp_create", "tk_decomp_destroy", "tk_decomp_arnoldi_sweeps",

@@ -108,3 +108,39 @@ def test_fused_launch_end_to_end(ctx, monkeypatch):
         out[fuse] = conv
     for name in ("relative_residual_norm", "projected_residual_norm", "orthogonality_data"):
         assert np.array_equal(getattr(out["0"], name), getattr(out["1"], name)), name
+
+
+@pytest.mark.parametrize("odd", [True, False])
+def test_fused_record_read_mid_sweep_then_continue(ctx, monkeypatch, odd):
+    """ADVICE r5: fused handles alternate a step's partials between P1 and P1b by step parity;
+    the only reduce outside a fused launch is red_flush, which picks the buffer by j.  A grouped
+    fused handle whose records are read in the middle of an asynchronous run -- at an odd step
+    (P1b) and at an even one (P1) -- and that then keeps stepping (the next fused launch reduces
+    nothing: its pending reduce already ran) equals the separate-reduce handle bit for bit."""
+    tk = _tk()
+    n, d, K = 1 << 15, 4, 30
+    jr = 13 if odd else 14
+    out = {}
+    for fuse in (False, True):
+        monkeypatch.setenv("TKHIP_D1_FUSE", "1" if fuse else "0")
+        csc = tk.assemble_matrix(n, "ConvDiff")
+        rng = np.random.default_rng(77)
+        bs = [v / np.linalg.norm(v) for v in (rng.random(n) for _ in range(d))]
+        A = tk.DeviceMatrix(ctx, csc)
+        dev = tk.DeviceDecomposition(ctx, tk._lib.TK_ARNOLDI, d, 0, [A] * d, bs, K)
+        assert dev.factor_groups == 2
+        dev.init(False)
+        for j in range(K):
+            if j == jr:
+                mid = dev.step(j)             # a record out: red_flush + the bookkeeping now
+            else:
+                dev.step_async(j)
+        recs = dev.records(0, K + 1)
+        V = [dev.basis(f, 0, K + 1) for f in range(d)]
+        out[fuse] = (mid, recs, V)
+        dev.close()
+        A.close()
+    assert np.array_equal(out[False][0], out[True][0])
+    assert np.array_equal(out[False][1], out[True][1])
+    for f in range(d):
+        assert np.array_equal(out[False][2][f], out[True][2][f])
