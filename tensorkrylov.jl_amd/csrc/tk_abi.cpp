@@ -1432,13 +1432,11 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
         d.hl = mats[f]->hl;
         d.hu = mats[f]->hu;
         {
-            // overlapping windows of 256 rows owning 256 - 2(hl+hu); partial blocks a
-            // function of (n, hl, hu) only, each walking the same number of windows
+            // overlapping windows of 256 rows owning 256 - 2(hl+hu), one k_arn_d1 block (and
+            // one partial slot) each: a function of (n, hl, hu) only
             const int ws = 256 - 2 * (d.hl + d.hu);
             d.nwin = (int)((n + ws - 1) / ws);
-            const char* ew = getenv("TKHIP_D1_WPB");
-            const int wpb = TK_D1_ONEWIN ? 1 : (ew ? std::max(0, atoi(ew)) : 0);
-            d.npd = wpb >= 1 ? (d.nwin + wpb - 1) / wpb : (d.nwin + std::max(1, d.nwin / npcap) - 1) / std::max(1, d.nwin / npcap);
+            d.npd = d.nwin;
         }
         dc->npd = std::max(dc->npd, d.npd);
         d.nwl = lan_windows(n, d.hl, d.hu);
@@ -1536,7 +1534,6 @@ tk_status tk_decomp_create(tk_ctx* c, int method, int d_total, int first_factor,
     if (const char* eg = getenv("TKHIP_TEST_GROUP_DELAY_US")) dc->gdelay_us = std::max(0.0, atof(eg));
     if (const char* ek = TEST_ENV("TKHIP_TEST_SKIP")) dc->skip_mask = atoi(ek);
     if (const char* eb = getenv("TKHIP_BK_FOLD")) dc->bk_fold = eb[0] != '0';
-    dc->bk_fold = dc->bk_fold && TK_D1_ONEWIN;   // (the window-loop kernel has no bookkeeping blocks)
     const char* xa = getenv("TKHIP_EXCHANGE_ALWAYS");
     if (has_peers(c) && (c->nranks > 1 || (xa && xa[0] == '1'))) {
         DA(dc->recv, (size_t)(kmax + 2) * d_total * dc->m * sizeof(double));

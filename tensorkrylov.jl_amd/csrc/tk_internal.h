@@ -160,11 +160,6 @@ __host__ __device__ inline int d1_nv(int J, int track_gram) { return track_gram 
 #define D1S_GAMMA 1
 #define D1S_BETA 2
 #define D1S_T1 3
-// 1: each k_arn_d1 block takes one window (DFac::npd == nwin); 0: blocks walk windows
-// (TKHIP_D1_WPB per block; 0 = about 1024 blocks per factor)
-#ifndef TK_D1_ONEWIN
-#define TK_D1_ONEWIN 1
-#endif
 
 // launchers (tk_kernels.hip)
 void launch_mirror_records(const double* src, double* dst, int cnt, unsigned long long* done, int nslots,

@@ -959,25 +959,16 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #ifndef TK_D1_L3
 #define TK_D1_L3 56
 #endif
-// Column dots: per window each 16-lane row of a wave reduce-scatters its products (rs16)
-// and every lane adds its result into a private LDS slot -- no barrier; the slots are
-// combined once, after the last window.  Chunk k < NUZ holds columns 8k..8k+7 times
-// (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row (16 columns
-// each).  acc[chunk][256]: slot t = (16-row group p = t >> 4, value s = t & 15).
-// Column-dot accumulation of k_arn_d1: rs64 (whole-wave reduce-scatter; the 16 values of a
-// chunk land in 4 wave slots) or rs16 (16-lane rows; 16 row-group slots per chunk)
-#ifndef TK_D1_RS64
-#define TK_D1_RS64 1
-#endif
-#ifndef TK_D1_SWPIN
-#define TK_D1_SWPIN 1
-#endif
+// Column dots: each wave reduce-scatters its products over all 64 lanes (rs64; the 16 values
+// of a chunk land in 4 lanes) and every fourth lane adds its result into a private LDS slot --
+// no barrier; the slots are combined once, at the end.  Chunk k < NUZ holds columns
+// 8k..8k+7 times (u, z) interleaved, chunk NUZ the six scalars, chunks NUZ+1.. the Gram row
+// (16 columns each).  acc[chunk][64]: slot = (wave p, value s).
 #define D1_ACC_Y(k, y)                                                                  \
     do {                                                                                \
         const double r_ = rs64_tail(y);                                                 \
         if ((t & 3) == 0) acc[(k) * 64 + (t >> 6) * 16 + ((t >> 2) & 15)] += r_;        \
     } while (0)
-#if TK_D1_RS64
 #define D1_ACC(k, x)                                                                    \
     do {                                                                                \
         const double r_ = rs64(x);                                                      \
@@ -986,12 +977,6 @@ __device__ __forceinline__ int clamp_row(int64_t i) { return i < 0 ? 0 : (i >= T
 #define D1_NP 4
 #define D1_CHW 64
 #define D1_PART(k, p, sl) acc[(k) * 64 + (p) * 16 + (sl)]
-#else
-#define D1_ACC(k, x) acc[(k) * TPB + t] += rs16(x)
-#define D1_NP 16
-#define D1_CHW TPB
-#define D1_PART(k, p, sl) acc[(k) * TPB + (p) * 16 + (sl)]
-#endif
 #if TK_D1_TRACE
 // diagnostic builds only (tools/build_variant.sh NAME - -DTK_D1_TRACE=1, tools/d1_trace.py):
 // per-block start / end wall clock (100 MHz) and HW_ID / XCC_ID of one step's k_arn_d1
@@ -1014,21 +999,10 @@ template <bool MM, bool FUSED>
 __device__ __forceinline__ void red256_block(const DFac& d, int fidx, int c, int which, int nv, int np, int coefJ,
                                              const KArgs& ax, unsigned long long wseq);
 __device__ void post_signal(const KArgs& a, const DFac& d, int fidx, bool mirrored, bool coherent = false);
+// narrow rows leave registers for more waves: the tiers rs64's register count allows (one
+// more wave per SIMD spills: -30..-45 %)
+#define D1_OCC (MAXC <= 8 ? 8 : (MAXC <= 16 ? 6 : (MAXC <= 24 ? 5 : (MAXC <= TK_D1_L4 ? 4 : (MAXC <= TK_D1_L3 ? 3 : 2)))))
 template <int MAXC, int FMT, int MODE>
-#ifndef TK_D1_OCCT
-#define TK_D1_OCCT 2
-#endif
-#if TK_D1_OCCT
-// narrow rows leave registers for more waves: 7 / 5 waves per SIMD at 8 / 16 columns
-#if TK_D1_OCCT == 2   // the tiers rs64's lower register count allows (one more spills: -30..-45 %)
-#define D1_RC MAXC
-#define D1_OCC (D1_RC <= 8 ? 8 : (D1_RC <= 16 ? 6 : (D1_RC <= 24 ? 5 : (D1_RC <= TK_D1_L4 ? 4 : (D1_RC <= TK_D1_L3 ? 3 : 2)))))
-#else
-#define D1_OCC (MAXC <= 8 ? 7 : (MAXC <= 16 ? 5 : OCC_WAVES(TK_D1_L4, TK_D1_L3)))
-#endif
-#else
-#define D1_OCC OCC_WAVES(TK_D1_L4, TK_D1_L3)
-#endif
 __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_OCC))) void k_arn_d1(const DFac* __restrict__ F, KArgs a,
                                                                                                   KArgs b) {
     constexpr int NUZ = MAXC / 8, NG = (MAXC + 15) / 16;
@@ -1041,11 +1015,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     // Bit 2 (WSC, one stream only): the previous step's reduce was a plain reduction -- wave 0
     // evaluates the step's scalars (d1_scalars) and hands them to the block through LDS
     constexpr bool WSC = (MODE & 4) != 0 && !FUSE;
-    __shared__ double xs[TK_D1_ONEWIN ? 2 : 4][TPB];   // u_j, u_{j+1} (by window parity)
+    __shared__ double xs[2][TPB];                      // u_j, u_{j+1}
     __shared__ double d1s[2];                          // the step's ib, gamma (wave 0 -> the block; WSC)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const DFac& d = F[blockIdx.y];
-#if TK_D1_ONEWIN
     // XCD-aware slot: workgroups are dispatched round-robin over the 8 XCDs, so block x runs
     // on XCD x % 8 (gridDim.x is a multiple of 8); each XCD takes a contiguous range of
     // windows -- neighbouring windows share halo rows in its L2 and its partial stores
@@ -1084,10 +1057,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const int bx = (int)blockIdx.x - x0;
     const int slot = (bx & 7) * (((int)gridDim.x - x0) >> 3) + (bx >> 3);
     if (slot >= d.nwin) return;
-#else
-    if ((int)blockIdx.x >= d.npd) return;
-    const int slot = blockIdx.x;
-#endif
 #if TK_D1_TRACE
     const uint64_t trace_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1111,14 +1080,9 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     const bool pg = !FUSE && a.pgrp;
     const int nvp = pg ? d1_groups(d1_nv(j + 1, gram)) * D1G : 0;
     for (int e = t; e < nvp; e += TPB) pv[e] = 0.0;
-    int par = 0;
-#if TK_D1_ONEWIN
     // one window per block (no window loop: nothing loop-invariant to hoist)
     {
         const int w = slot;
-#else
-    for (int w = blockIdx.x; w < d.nwin; w += d.npd, par ^= 1) {
-#endif
         const int64_t S = (int64_t)w * WS - 2 * hl;
         const int64_t r = S + t;
         const bool inb = r >= 0 && r < a.ld;
@@ -1138,8 +1102,8 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // first) and every wave evaluates them (d1_scalars); step 0 reads the init's
         const int l = t & 63;
         double cl0 = 0.0, ql0 = 0.0;
-        double* xv = xs[par];
-        double* xu = xs[TK_D1_ONEWIN ? 1 : 2 + par];
+        double* xv = xs[0];
+        double* xu = xs[1];
         // u_j (and column j-1 from E) first, then the basis row: A u_j needs only u_j, so the
         // first SpMV (its barrier and LDS reads) runs while the row's loads are in flight, and
         // the row is waited for at the projections row . c, row . q that follow (round 6, same
@@ -1225,7 +1189,6 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         // update_rhs!'s <v_j, b> as norm(b) * <v_j, v_0> (b = norm(b) v_0, src/decompositions.jl:
         // 112-118): v_0 is column 0 of the register row, so b is not read (-8 B per row)
 #define D1_V0R (j > 0 ? R.v[0] : vj)   // (read where used)
-#if TK_D1_RS64 && TK_D1_SWPIN
         // rs64's first step on the inputs: the basis entries of columns c and c+4 are
         // half-exchanged once for the u, the z and the Gram products, and each lane forms its
         // half's two-lane sums as one product and one FMA (the partner's u, z, v come from one
@@ -1263,43 +1226,12 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             }
             if (gram && 16 * g < j) D1_ACC_Y(NUZ + 1 + g, yg);
         }
-#else
-#pragma unroll
-        for (int k = 0; k < NUZ; ++k) {
-            if (8 * k < j) {
-                double x[16];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    x[2 * i] = R.v[8 * k + i] * uo;
-                    x[2 * i + 1] = R.v[8 * k + i] * zo;
-                }
-                D1_ACC(k, x);
-            }
-        }
-        if (gram) {
-#pragma unroll
-            for (int k = 0; k < NG; ++k) {
-                if (16 * k < j) {
-                    double x[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) x[i] = 16 * k + i < MAXC ? R.v[16 * k + i < MAXC ? 16 * k + i : 0] * vo : 0.0;
-                    D1_ACC(NUZ + 1 + k, x);
-                }
-            }
-        }
-#endif
         {
-#if TK_D1_RS64 && TK_D1_SWPIN
             // the six scalars in value slots 0..2 (lower half-wave) and 8..10 (upper): three
             // cross-half exchanges, the rest of the first step is zeros
             const double v0r = D1_V0R;
             double y[8] = {swap_add32(vo * u, uo * z), swap_add32(vo * z, vo * v0r), swap_add32(uo * u, vo * vj)};
             D1_ACC_Y(NUZ, y);
-#else
-            const double v0r = D1_V0R;
-            double x[16] = {vo * u, vo * z, uo * u, uo * z, vo * v0r, vo * vj};
-            D1_ACC(NUZ, x);
-#endif
         }
     }
     // combine the row-group partials of every value (fixed order) -> P1, in the layout the
@@ -1317,18 +1249,11 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
             const int col = 8 * k + (sl >> 1);
             if (col < j) vi = (sl & 1) ? j + 1 + col : col;
         } else if (k == NUZ) {
-#if TK_D1_RS64 && TK_D1_SWPIN
             if ((sl & 7) < 3) vi = sl == 0 ? j : 2 * j + (sl < 8 ? sl : sl - 5);   // slots 0,1,2 | 8,9,10
-#else
-            if (sl < 6) vi = sl == 0 ? j : 2 * j + sl;
-#endif
         } else {
-#if TK_D1_RS64 && TK_D1_SWPIN   // slot sl of Gram chunk g: pair q = sl & 3 of column chunk
-                                // 2g + bit 2, upper column (+4) for bit 3
+            // slot sl of Gram chunk g: pair q = sl & 3 of column chunk 2g + bit 2, upper
+            // column (+4) for bit 3
             const int col = 16 * (k - NUZ - 1) + (sl & 3) + 8 * ((sl >> 2) & 1) + 4 * ((sl >> 3) & 1);
-#else
-            const int col = 16 * (k - NUZ - 1) + sl;
-#endif
             if (col < j) vi = 2 * j + 6 + col;
         }
         if (vi >= 0) {
@@ -3157,7 +3082,7 @@ void launch_arn_d1(const DFac* F, int nf, const KArgs& a0, const KArgs& b, int n
     if (b.j >= 0) lds = std::max(lds, bk_lds_doubles(b.j) * sizeof(double));
     // (fused with a pending reduce: nf * (3j + 3) leading reducer blocks, rounded to whole XCD rounds)
     const int xr = (fuse && a.red) ? (nf * (3 * a.j + 3) + 7) & ~7 : 0;
-    const int gx = TK_D1_ONEWIN ? xr + (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0) : npd;
+    const int gx = xr + (npd + 7) / 8 * 8 + (b.j >= 0 ? 8 : 0);
     with_band_fmt(a.fmt, [&](auto FM) {
         with_maxc(a.j, [&](auto M) {
             constexpr int MV = decltype(M)::value, FV = decltype(FM)::value;
