@@ -988,7 +988,7 @@ __device__ uint64_t g_trace_ph[4 * TRACE_MAX];   // phase clocks (loads done, Sp
 #define D1_PHASE(k)                                                                   \
     do {                                                                              \
         __builtin_amdgcn_s_waitcnt(0);                                                \
-        if (t == 0 && blockIdx.y == 0 && j == g_trace_j && slot < TRACE_MAX)          \
+        if (t == 0 && d.gidx == 0 && j == g_trace_j && slot < TRACE_MAX)          \
             g_trace_ph[4 * slot + (k)] = __builtin_amdgcn_s_memrealtime();            \
     } while (0)
 #else
@@ -1272,7 +1272,7 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
     }
 #if TK_D1_TRACE
     __syncthreads();
-    if (t == 0 && blockIdx.y == 0 && j == g_trace_j && slot < TRACE_MAX) {
+    if (t == 0 && d.gidx == 0 && j == g_trace_j && slot < TRACE_MAX) {
         g_trace[3 * slot] = trace_t0;
         g_trace[3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
         g_trace[3 * slot + 2] = ((uint64_t)__builtin_amdgcn_s_getreg(63508) << 32) | __builtin_amdgcn_s_getreg(63492);

@@ -58,6 +58,14 @@ def main():
             rel = (ph.astype(np.float64) - tr[:, :1].astype(np.float64)) / 100.0
             print("  phases (median us from block start): loads %.2f  spmv1 %.2f  spmv2 %.2f  dots %.2f  end %.2f"
                   % (*np.median(rel, axis=0), np.median(du)))
+        # the XCD-aware slot map assumes the dispatcher deals blocks round-robin over the XCDs, so
+        # slot range s // ceil(nwin / 8) runs on one XCD (XCC_ID numbers them in another order):
+        # the share of each range's blocks on its most common XCD
+        slots = np.nonzero(keep)[0]
+        per = max(1, (len(tr) + 7) // 8)
+        rng = slots // per
+        held = sum(np.bincount(xcc[rng == r], minlength=16).max() for r in np.unique(rng))
+        print("  slot ranges of %d on one XCD: %.1f %% of blocks" % (per, 100.0 * held / len(tr)))
         grid = np.arange(0, en.max() + 1.0, 1.0)
         act = [int(((st <= g) & (en > g)).sum()) for g in grid]
         print("  active blocks per us:", " ".join(str(a) for a in act))
