@@ -129,6 +129,17 @@ __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(OCC(MAXC), O
         }
 }
 
+// a stand-in for the step's reduce: block (c, f) sums value c's npd window partials
+__global__ __launch_bounds__(256) void k_red_probe(const Fac* __restrict__ F, int npd, double* out) {
+    const double* P = F[blockIdx.y].P + (int64_t)blockIdx.x * npd;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < npd; b += 256) s += __builtin_nontemporal_load(P + b);
+    if (s == 12345.678) out[blockIdx.x] = s;   // (never: keeps the loads)
+}
+static void launch_red(const Fac* F, int nf, int nv, int npd, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_red_probe, dim3(nv, nf), dim3(256), 0, s, F, npd, out);
+}
+
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
 static int g_var = 0, g_bs = 256;
@@ -183,18 +194,29 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     CK(hipEventCreateWithFlags(&jn, hipEventDisableTiming));
+    hipEvent_t ea, eb;
+    CK(hipEventCreateWithFlags(&ea, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
+    CK(hipEventRecord(eb, s1));
+    hipEvent_t ra, rb;
+    CK(hipEventCreateWithFlags(&ra, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&rb, hipEventDisableTiming));
+    CK(hipEventRecord(ra, s1));
+    CK(hipEventRecord(rb, s1));
+    double* dout;
+    CK(hipMalloc(&dout, 4096 * sizeof(double)));
     const int nvar = argc > 4 ? argc - 4 : 1;
     printf("n=%ld nf=%d kmax=%d windows=%d (per-step algorithmic bytes 8n(j+3) per factor; TB/s)\n", (long)n, nf,
            kmax, nwin);
     for (int vi = 0; vi < nvar; ++vi) {
         g_var = argc > 4 ? atoi(argv[4 + vi]) : 0;
-        printf("variant %d: %4s %4s %16s %16s %16s %16s\n", g_var, "j", "MAXC", "1 launch", "2 groups+join",
-               "2 groups", "loads only");
+        printf("variant %d: %4s %4s %16s %16s %16s %16s %16s %16s %16s %16s\n", g_var, "j", "MAXC", "1 launch", "2 groups+join",
+               "2 groups", "loads only", "2 in sequence", "2 turns (events)", "seq + side reduces", "groups + reduces");
         for (int j = 4; j < kmax && j <= 63; j += 4) {
             const int M = j < 8 ? 8 : ((j + 7) / 8) * 8;
             const double bytes = 8.0 * n * (j + 3) * nf;
-            float ms[4];
-            for (int mode = 0; mode < 4; ++mode) {
+            float ms[8];
+            for (int mode = 0; mode < 8; ++mode) {
                 auto run = [&] {
                     if (mode == 1 || mode == 2) {
                         if (mode == 1) {
@@ -209,6 +231,42 @@ int main(int argc, char** argv) {
                         }
                     } else if (mode == 0) {
                         launch<true>(M, F, nf, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                    } else if (mode == 4) {
+                        // (the two groups' launches one after the other: groups taking turns)
+                        launch<true>(M, F, nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        launch<true>(M, F + nf / 2, nf - nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                    } else if (mode == 5) {
+                        // (the same order from two streams: each launch waits for the other
+                        // stream's last launch through an event, as factor groups taking turns)
+                        CK(hipStreamWaitEvent(s0, eb, 0));
+                        launch<true>(M, F, nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        CK(hipEventRecord(ea, s0));
+                        CK(hipStreamWaitEvent(s1, ea, 0));
+                        launch<true>(M, F + nf / 2, nf - nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s1);
+                        CK(hipEventRecord(eb, s1));
+                    } else if (mode == 6) {
+                        // sweeps back to back on one stream; each group's reduce on the side
+                        // stream behind its sweep, and the group's next sweep behind that reduce
+                        const int nv = 3 * j + 6;
+                        CK(hipStreamWaitEvent(s0, ra, 0));
+                        launch<true>(M, F, nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        CK(hipEventRecord(ea, s0));
+                        CK(hipStreamWaitEvent(s1, ea, 0));
+                        launch_red(F, nf / 2, nv, npd, dout, s1);
+                        CK(hipEventRecord(ra, s1));
+                        CK(hipStreamWaitEvent(s0, rb, 0));
+                        launch<true>(M, F + nf / 2, nf - nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        CK(hipEventRecord(eb, s0));
+                        CK(hipStreamWaitEvent(s1, eb, 0));
+                        launch_red(F + nf / 2, nf - nf / 2, nv, npd, dout, s1);
+                        CK(hipEventRecord(rb, s1));
+                    } else if (mode == 7) {
+                        // today's factor groups: each group's sweep and reduce on its own stream
+                        const int nv = 3 * j + 6;
+                        launch<true>(M, F, nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        launch_red(F, nf / 2, nv, npd, dout, s0);
+                        launch<true>(M, F + nf / 2, nf - nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s1);
+                        launch_red(F + nf / 2, nf - nf / 2, nv, npd, dout, s1);
                     } else {
                         launch<false>(M, F, nf, n, ld, ntiles, kmax, j, nwin, npd, s0);
                     }
@@ -228,7 +286,7 @@ int main(int argc, char** argv) {
                 ms[mode] = t / reps;
             }
             printf("           %4d %4d", j, M);
-            for (int mode = 0; mode < 4; ++mode)
+            for (int mode = 0; mode < 8; ++mode)
                 printf(" %8.1f us %5.2f", ms[mode] * 1e3, bytes / (ms[mode] * 1e-3) / 1e12);
             printf("\n");
         }
