@@ -42,10 +42,23 @@ struct Fac {
 // 8 u / v / E with plain stores
 template <int MAXC, bool STORE, int BS>
 __global__ __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(OCC(MAXC), OCC(MAXC)))) void k_probe(
-    const Fac* __restrict__ F, int64_t n, int64_t ld, int ntiles, int kmax, int j, int nwin, int npd, int var) {
+    const Fac* __restrict__ F, int64_t n, int64_t ld, int ntiles, int kmax, int j, int nwin, int npd, int var,
+    int xx = 0, int xoff = 0, int xnv = 0) {
     const Fac& d = F[blockIdx.y];
-    const int bx = blockIdx.x;
-    const int slot = (bx & 7) * ((int)gridDim.x >> 3) + (bx >> 3);
+    // (xx > 0: leading blocks sum the npd partials of value x of factor F[xoff + y] first -- the
+    // other group's reduce inside this launch)
+    if ((int)blockIdx.x < xx) {
+        if ((int)blockIdx.x < xnv) {
+            const Fac& xd = F[xoff + (int)blockIdx.y];   // (xoff < 0 for the second group: int arithmetic)
+            const double* P = xd.P + (int64_t)blockIdx.x * npd;
+            double s = 0.0;
+            for (int b = threadIdx.x; b < npd; b += BS) s += __builtin_nontemporal_load(P + b);
+            if (s == 12345.678) st_wt(xd.P, 0, s);
+        }
+        return;
+    }
+    const int bx = (int)blockIdx.x - xx;
+    const int slot = (bx & 7) * (((int)gridDim.x - xx) >> 3) + (bx >> 3);
     if (slot >= nwin) return;
     const int t = threadIdx.x, hl = 1, hu = 1, WS = BS - 2 * (hl + hu);
     const int64_t TS = (int64_t)TPB * ((kmax + 2) & ~1);
@@ -143,12 +156,14 @@ static void launch_red(const Fac* F, int nf, int nv, int npd, double* out, hipSt
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
 static int g_var = 0, g_bs = 256;
+static int g_xoff = 0, g_xnv = 0;   // (mode 8: the other group's reduce in the leading blocks)
 template <bool STORE, int BS>
 static void launch_bs(int M, const Fac* F, int nf, int64_t n, int64_t ld, int ntiles, int kmax, int j, int npd,
                       hipStream_t s) {
     const int nwin = (int)((n + (BS - 4) - 1) / (BS - 4));
-    dim3 g((nwin + 7) & ~7, nf);
-#define L_(MM) case MM: hipLaunchKernelGGL((k_probe<MM, STORE, BS>), g, dim3(BS), 0, s, F, n, ld, ntiles, kmax, j, nwin, npd, g_var); break;
+    const int xx = (g_xnv + 7) & ~7;
+    dim3 g(xx + ((nwin + 7) & ~7), nf);
+#define L_(MM) case MM: hipLaunchKernelGGL((k_probe<MM, STORE, BS>), g, dim3(BS), 0, s, F, n, ld, ntiles, kmax, j, nwin, npd, g_var, xx, g_xoff, g_xnv); break;
     switch (M) { L_(8) L_(16) L_(24) L_(32) L_(40) L_(48) L_(56) L_(64) }
 #undef L_
 }
@@ -210,13 +225,14 @@ int main(int argc, char** argv) {
            kmax, nwin);
     for (int vi = 0; vi < nvar; ++vi) {
         g_var = argc > 4 ? atoi(argv[4 + vi]) : 0;
-        printf("variant %d: %4s %4s %16s %16s %16s %16s %16s %16s %16s %16s\n", g_var, "j", "MAXC", "1 launch", "2 groups+join",
-               "2 groups", "loads only", "2 in sequence", "2 turns (events)", "seq + side reduces", "groups + reduces");
+        printf("variant %d: %4s %4s %16s %16s %16s %16s %16s %16s %16s %16s %16s\n", g_var, "j", "MAXC", "1 launch", "2 groups+join",
+               "2 groups", "loads only", "2 in sequence", "2 turns (events)", "seq + side reduces", "groups + reduces",
+               "seq + in-launch reduces");
         for (int j = 4; j < kmax && j <= 63; j += 4) {
             const int M = j < 8 ? 8 : ((j + 7) / 8) * 8;
             const double bytes = 8.0 * n * (j + 3) * nf;
-            float ms[8];
-            for (int mode = 0; mode < 8; ++mode) {
+            float ms[9];
+            for (int mode = 0; mode < 9; ++mode) {
                 auto run = [&] {
                     if (mode == 1 || mode == 2) {
                         if (mode == 1) {
@@ -260,6 +276,16 @@ int main(int argc, char** argv) {
                         CK(hipStreamWaitEvent(s1, eb, 0));
                         launch_red(F + nf / 2, nf - nf / 2, nv, npd, dout, s1);
                         CK(hipEventRecord(rb, s1));
+                    } else if (mode == 8) {
+                        // groups taking turns on one stream, each launch reducing the other group's
+                        // last sweep in its leading blocks
+                        g_xnv = 3 * j + 6;
+                        g_xoff = nf / 2;
+                        launch<true>(M, F, nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        g_xoff = -(nf / 2);
+                        launch<true>(M, F + nf / 2, nf - nf / 2, n, ld, ntiles, kmax, j, nwin, npd, s0);
+                        g_xnv = 0;
+                        g_xoff = 0;
                     } else if (mode == 7) {
                         // today's factor groups: each group's sweep and reduce on its own stream
                         const int nv = 3 * j + 6;
@@ -286,7 +312,7 @@ int main(int argc, char** argv) {
                 ms[mode] = t / reps;
             }
             printf("           %4d %4d", j, M);
-            for (int mode = 0; mode < 8; ++mode)
+            for (int mode = 0; mode < 9; ++mode)
                 printf(" %8.1f us %5.2f", ms[mode] * 1e3, bytes / (ms[mode] * 1e-3) / 1e12);
             printf("\n");
         }
