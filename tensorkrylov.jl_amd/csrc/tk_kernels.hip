@@ -1037,6 +1037,10 @@ __global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(D1_OCC, D1_
         if (blockIdx.y == 0 && f < (int)gridDim.y) {
             // step j-1's reduce (k_reduce256's block; its last block evaluates this step's scalars)
             const int jp = a.j - 1;
+            // (a.red implies j >= 1: red256_block's one-sweep Lanczos branch, coefJ == RED_LAN, is
+            // then dead code -- without this the compiler kept it, and its 20 B/lane of scratch
+            // memory made every fused instantiation a scratch-using kernel)
+            __builtin_assume(jp >= 0);
             if (a.redmm) red256_block<true, true>(F[f], f, c, (jp & 1) ? 5 : 1, 3 * jp + 6, 0, jp + 1, a, a.wseq);
             else red256_block<false, true>(F[f], f, c, (jp & 1) ? 5 : 1, 3 * jp + 6, 0, jp + 1, a, a.wseq);
         }
